@@ -1,0 +1,211 @@
+#!/usr/bin/env python3
+"""bench.py — the BASELINE.json metric on MI355X.
+
+    python bench.py [--gpus N --steps K --warmup W]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+Metric: scored (positive + negative) triples per second of the training step,
+RotatE FB15k shape (E=14951, R=1345) d=1000 -de, b=1024 per GPU, n=256,
+self-adversarial (T=1.0), γ=24 — BASELINE config 2 (best_config.sh:3).
+One step = KGEModel.train_step exactly as run.py calls it: fused scoring + loss +
+backward (libkge_hip.so) + KGEAdam dense update + the loss read-back, with
+batches pre-staged in HBM (the CPU sampler cannot feed this rate; SURVEY §7 v)
+and alternating tail-/head-batch like BidirectionalOneShotIterator.
+Data: synthetic (uniform ids, reference init U(-range, range) tables).
+
+Prints one JSON line (rank 0).  `roofline` is the dominant kernel (the fused
+row pass) timed live with HIP events on its launch stream; `cpu_baseline` is
+the oracle's ATen op chain (the reference's algorithm) on this host.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from argparse import Namespace
+
+import torch
+import torch.distributed as dist
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+from knowledgegraphembedding_amd import KGEAdam, KGEModel, _lib  # noqa: E402
+
+E, R, D, B, NNEG, GAMMA, TEMP = 14951, 1345, 1000, 1024, 256, 24.0, 1.0
+METRIC = "scored (pos+neg) triples/sec, RotatE FB15k d=1000 b=1024 n=256, 1/2/4/8 GPU"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
+
+
+def algorithmic_row_bytes(b: int, n: int, le: int, lr: int) -> int:
+    """Bytes one fused row-pass launch must move: every negative
+    row once, the positive h/r/t rows, indices and weights."""
+    return b * n * le * 4 + b * (le + lr + le) * 4 + b * n * 8 + b * 3 * 8 + b * 4
+
+
+class DeviceBatches:
+    """Pre-staged device batches, tail-batch on odd steps and head-batch on even
+    steps (dataloader.py:171-177)."""
+
+    def __init__(self, dev, seed: int, nsets: int = 4):
+        g = torch.Generator(device=dev)
+        g.manual_seed(seed)
+        self.sets = []
+        for _ in range(nsets):
+            h = torch.randint(0, E, (B,), device=dev, generator=g)
+            r = torch.randint(0, R, (B,), device=dev, generator=g)
+            t = torch.randint(0, E, (B,), device=dev, generator=g)
+            pos = torch.stack([h, r, t], 1).contiguous()
+            neg = torch.randint(0, E, (B, NNEG), device=dev, generator=g)
+            w = torch.rand(B, device=dev, generator=g) * 0.3 + 0.1
+            self.sets.append((pos, neg, w))
+        self.step = 0
+
+    def __iter__(self):
+        return self
+
+    def __next__(self):
+        self.step += 1
+        pos, neg, w = self.sets[self.step % len(self.sets)]
+        return pos, neg, w, ('head-batch' if self.step % 2 == 0 else 'tail-batch')
+
+
+def cpu_baseline(model_cpu_state, budget_s: float = 12.0, b: int = 32):
+    """The oracle (reference op chain on CPU fp32, + torch.optim.Adam) on a
+    bounded sample of the same workload: b positives x 256 negatives."""
+    from oracle import kge_oracle as O
+    ent, rel, erange = model_cpu_state
+    g = torch.Generator().manual_seed(7)
+    pos = torch.stack([torch.randint(0, E, (b,), generator=g), torch.randint(0, R, (b,), generator=g),
+                       torch.randint(0, E, (b,), generator=g)], 1)
+    neg = torch.randint(0, E, (b, NNEG), generator=g)
+    w = torch.rand(b, generator=g) * 0.3 + 0.1
+    params = [ent.clone().requires_grad_(True), rel.clone().requires_grad_(True)]
+    opt = torch.optim.Adam(params, lr=1e-4)
+
+    def step(mode):
+        _, ge, gr, _ = O.train_grads("RotatE", params[0].detach(), params[1].detach(), None, pos, neg, w, mode,
+                                     adversarial=True, temperature=TEMP, uni_weight=False, regularization=0.0,
+                                     gamma=GAMMA, erange=erange)
+        opt.zero_grad()
+        params[0].grad, params[1].grad = ge, gr
+        opt.step()
+
+    step('tail-batch')  # warm-up
+    t0 = time.perf_counter()
+    k = 0
+    while True:
+        step('head-batch' if k % 2 else 'tail-batch')
+        k += 1
+        if time.perf_counter() - t0 > budget_s or k >= 16:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": k * b * (NNEG + 1) / dt, "unit": "triples/s", "cores": torch.get_num_threads(),
+            "kind": "port",
+            "sample": f"oracle train step (ATen op chain fwd + autograd bwd + torch Adam), RotatE E={E} R={R} "
+                      f"d={D} b={b} n={NNEG} adv, {k} timed steps after 1 warm-up, {dt:.1f} s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=12.0)
+    ap.add_argument("--traffic-json", default=None,
+                    help="rocprofv3 PMC summary (tools/pmc_traffic.py output) for roofline.traffic")
+    a = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    group = None
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+        group = dist.group.WORLD
+
+    torch.manual_seed(0)
+    model = KGEModel("RotatE", E, R, D, GAMMA, double_entity_embedding=True, double_relation_embedding=False)
+    erange = model.embedding_range.item()
+    cpu_state = (model.entity_embedding.detach().clone(), model.relation_embedding.detach().clone(), erange)
+    model = model.to(dev)
+    args = Namespace(cuda=True, negative_adversarial_sampling=True, adversarial_temperature=TEMP, uni_weight=False,
+                     regularization=0.0, dp_group=group)
+    opt = KGEAdam([p for p in model.parameters() if p.requires_grad], lr=1e-4)
+    it = DeviceBatches(dev, seed=1000 + rank)
+
+    for _ in range(a.warmup):
+        KGEModel.train_step(model, opt, it, args)
+    torch.cuda.synchronize()
+
+    lib = _lib.load()
+    _lib.check(lib.kge_stage_timer(1, None, 0), "kge_stage_timer")
+    if group is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        KGEModel.train_step(model, opt, it, args)
+    torch.cuda.synchronize()
+    if group is not None:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    stage = (torch.zeros(5, dtype=torch.float32)).numpy()
+    import ctypes
+    _lib.check(lib.kge_stage_timer(2, stage.ctypes.data_as(ctypes.c_void_p), 5), "kge_stage_timer")
+    lib.kge_stage_timer(0, None, 0)
+    if group is not None:
+        t = torch.tensor([dt], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+
+    calls = max(1.0, float(stage[4]))
+    row_ms = float(stage[0]) / calls
+    row_bytes = algorithmic_row_bytes(B, NNEG, 2 * D, D)
+    achieved = row_bytes / (row_ms * 1e-3) / 1e9
+    traffic = None
+    if a.traffic_json and os.path.exists(a.traffic_json):
+        with open(a.traffic_json) as f:
+            traffic = json.load(f).get("hbm_bytes_per_launch")
+
+    value = a.steps * B * (NNEG + 1) * world / dt
+    out = {
+        "metric": METRIC,
+        "value": value,
+        "unit": "triples/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": dt / a.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "fp32",
+        "data": "synthetic (uniform ids, U(-range,range) tables), batches pre-staged in HBM",
+        "config": {"workload": "RotatE FB15k-shape train_step (fused score+self-adv loss+bwd, dense Adam)",
+                   "entities": E, "relations": R, "hidden_dim": D, "batch_per_gpu": B, "global_batch": B * world,
+                   "negatives": NNEG, "adversarial_temperature": TEMP, "gamma": GAMMA,
+                   "parallelism": f"dp{world}"},
+        "stage_ms": {"row_pass": row_ms, "csr": float(stage[1]) / calls, "entity_pass": float(stage[2]) / calls,
+                     "relation_pass_finalize": float(stage[3]) / calls,
+                     "other_incl_adam_ms": dt / a.steps * 1e3 - float(stage[:4].sum()) / calls},
+        "roofline": {"bound": "hbm", "kernel": "k_row (fused negative scoring + self-adversarial loss)",
+                     "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                     "traffic": traffic, "algorithmic_bytes_per_launch": row_bytes,
+                     "avg_launch_ms": row_ms},
+    }
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(cpu_state, budget_s=a.cpu_budget)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if group is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,194 @@
+/*
+ * kge_hip.h — C-ABI of the MI355X (gfx950) knowledge-graph-embedding hot path.
+ *
+ * Drop-in boundary for the scoring / self-adversarial-loss / filtered-ranking
+ * path of kahrabian/KnowledgeGraphEmbedding.  The reference has no FFI: its
+ * boundary is the Python methods of `KGEModel` (codes/model.py).  Each entry
+ * point below names the reference interface it replaces (file:line); the
+ * Python host mirror in knowledgegraphembedding_amd/ binds these through
+ * ctypes (see INTEGRATION.md for the binding a reference maintainer would add).
+ *
+ * Conventions
+ *   - All array arguments are DEVICE pointers (hipMalloc / torch CUDA tensors),
+ *     row-major and contiguous.  Embeddings are fp32, indices int64 — the
+ *     reference's own dtypes (model.py:45,52; dataloader.py:63-65).
+ *   - `stream` is a hipStream_t passed as void* (NULL = default stream).
+ *     Nothing here allocates, frees or synchronises: every call is
+ *     graph-capturable.  Scratch comes from a caller-owned workspace whose
+ *     size the matching *_workspace_bytes() query returns.
+ *   - Return value: 0 on success, a KGE_ERR_* code for argument errors
+ *     (checked on the host before anything is launched), or a hipError_t
+ *     (offset by KGE_ERR_HIP_BASE) if a launch fails.
+ *   - Index range errors (reference: index_select raises, model.py:86-146)
+ *     cannot be checked on the host without a sync; kernels clamp nothing,
+ *     skip the offending row, and set *err_flag (a device int32) to
+ *     KGE_DEVERR_INDEX.  The host mirror reads the flag at its next sync
+ *     point and raises IndexError.
+ */
+#ifndef KGE_HIP_H
+#define KGE_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Model ids: model.py:151-157 (the model_func plug-in registry). */
+enum kge_model_id {
+    KGE_TRANSE = 0,   /* model.py:166-173 */
+    KGE_DISTMULT = 1, /* model.py:175-182 */
+    KGE_COMPLEX = 2,  /* model.py:184-199 */
+    KGE_ROTATE = 3,   /* model.py:201-229 */
+    KGE_PROTATE = 4   /* model.py:231-249 */
+};
+
+/* Modes: model.py:83 'single', :104 'head-batch', :126 'tail-batch'. */
+enum kge_mode_id { KGE_SINGLE = 0, KGE_HEAD_BATCH = 1, KGE_TAIL_BATCH = 2 };
+
+enum kge_status {
+    KGE_OK = 0,
+    KGE_ERR_MODEL = 1,      /* ValueError('model %s not supported'), model.py:64,162 */
+    KGE_ERR_MODE = 2,       /* ValueError('mode %s not supported'), model.py:149 */
+    KGE_ERR_SHAPE = 3,      /* entity/relation dims inconsistent with the model (model.py:66-70) */
+    KGE_ERR_ARG = 4,        /* null pointer / negative size */
+    KGE_ERR_WORKSPACE = 5,  /* workspace smaller than *_workspace_bytes() */
+    KGE_ERR_DIM = 6,        /* row length beyond what the kernels are instantiated for */
+    KGE_ERR_HIP_BASE = 1000 /* + hipError_t */
+};
+
+/* Device-side error bits written to *err_flag. */
+#define KGE_DEVERR_INDEX 1
+
+/*
+ * The parameters of one KGEModel (model.py:22-70).
+ *   phase_divisor   = float(embedding_range.item() / 3.14159265358979323846)  model.py:202,209
+ *   phase_divisor_p = float(embedding_range.item() / 3.14159262358979323846)  model.py:232,236-238
+ *                     (the reference's pi typo is part of the contract)
+ *   modulus         = device pointer to the pRotatE [1,1] modulus (model.py:59-60), else NULL
+ */
+typedef struct kge_model_desc {
+    int32_t model;
+    int32_t entity_dim;   /* floats per entity row   (model.py:42) */
+    int32_t relation_dim; /* floats per relation row (model.py:43) */
+    int32_t reserved;
+    int64_t nentity;
+    int64_t nrelation;
+    float gamma;          /* model.py:32-35 */
+    float phase_divisor;
+    float phase_divisor_p;
+    float reserved_f;
+    const float *entity_embedding;   /* [nentity, entity_dim] */
+    const float *relation_embedding; /* [nrelation, relation_dim] */
+    const float *modulus;            /* [1] or NULL */
+} kge_model_desc;
+
+/* Library identity (for the loader's symbol check). */
+const char *kge_version(void);
+const char *kge_status_string(int status);
+
+/*
+ * Scores of a batch — replaces KGEModel.forward(sample, mode) (model.py:72-164)
+ * together with the score plug-ins (model.py:166-249).
+ *   mode == KGE_SINGLE:      pos[batch,3] triples, neg ignored, nneg must be 1 → out[batch,1]
+ *   mode == KGE_HEAD_BATCH:  sample = (tail_part=pos[batch,3], head_part=neg[batch,nneg])
+ *   mode == KGE_TAIL_BATCH:  sample = (head_part=pos[batch,3], tail_part=neg[batch,nneg])
+ *   out: [batch, nneg] fp32.
+ */
+int kge_score(const kge_model_desc *m, int32_t mode, const int64_t *pos, const int64_t *neg,
+              int64_t batch, int64_t nneg, float *out, int32_t *err_flag, void *stream);
+
+/*
+ * Gradient of sum(grad_scores * score) w.r.t. the tables — replaces the autograd
+ * of KGEModel.forward (IndexSelectBackward = dense zero-fill + index_add_, then
+ * the plug-in's elementwise backward).
+ *   grad_entity [nentity, entity_dim], grad_relation [nrelation, relation_dim] are
+ *   OVERWRITTEN densely (rows no sample touches become 0); grad_modulus [1] is
+ *   overwritten when non-NULL (pRotatE).
+ */
+size_t kge_backward_workspace_bytes(const kge_model_desc *m, int32_t mode, int64_t batch, int64_t nneg);
+int kge_score_backward(const kge_model_desc *m, int32_t mode, const int64_t *pos, const int64_t *neg,
+                       int64_t batch, int64_t nneg, const float *grad_scores, float *grad_entity,
+                       float *grad_relation, float *grad_modulus, void *workspace, size_t workspace_bytes,
+                       int32_t *err_flag, void *stream);
+
+/*
+ * Fused negative scoring + self-adversarial logsigmoid loss + backward —
+ * replaces KGEModel.train_step (model.py:252-301) from the forward calls up to
+ * and including loss.backward(); the optimizer step stays separate (kge_adam_step).
+ *   mode:            KGE_HEAD_BATCH or KGE_TAIL_BATCH (dataloader.py:171-177 alternates them)
+ *   pos [batch,3], neg [batch,nneg], subsampling_weight [batch]
+ *   weight_sum:      device scalar Σw over the GLOBAL batch (data-parallel ranks all-reduce it);
+ *                    NULL = computed from subsampling_weight of this call.
+ *   uni_weight:      args.uni_weight (model.py:281-286)
+ *   uni_batch:       the global batch size used for the uni_weight means (0 = batch)
+ *   adversarial:     args.negative_adversarial_sampling; temperature = args.adversarial_temperature
+ *   regularization:  args.regularization (model.py:290-296); 0 disables
+ *   losses_out [4]:  {positive_sample_loss, negative_sample_loss, loss, regularization}
+ *                    (device fp32; the reference's log dict, model.py:305-310)
+ *   grad_* overwritten densely, as in kge_score_backward.
+ */
+size_t kge_train_workspace_bytes(const kge_model_desc *m, int64_t batch, int64_t nneg);
+int kge_train_step_grads(const kge_model_desc *m, int32_t mode, const int64_t *pos, const int64_t *neg,
+                         int64_t batch, int64_t nneg, const float *subsampling_weight,
+                         const float *weight_sum, int32_t uni_weight, int64_t uni_batch,
+                         int32_t adversarial, float adversarial_temperature, float regularization,
+                         float *grad_entity, float *grad_relation, float *grad_modulus,
+                         float *losses_out, void *workspace, size_t workspace_bytes,
+                         int32_t *err_flag, void *stream);
+
+/*
+ * Σ subsampling_weight into *out (device scalar) — the denominator of
+ * model.py:285-286; exposed so data-parallel ranks can all-reduce it.
+ */
+int kge_weight_sum(const float *w, int64_t n, float *out, void *stream);
+
+/*
+ * One dense Adam update — replaces torch.optim.Adam.step() as the reference
+ * uses it (run.py:266-269, model.py:303; betas/eps defaults, no weight decay,
+ * no amsgrad).  step_size = lr / (1 - beta1^t) and bias_correction2_sqrt =
+ * sqrt(1 - beta2^t) are computed by the caller in double, as torch does.
+ */
+int kge_adam_step(float *param, const float *grad, float *exp_avg, float *exp_avg_sq, int64_t numel,
+                  float beta1, float beta2, float eps, float step_size, float bias_correction2_sqrt,
+                  void *stream);
+
+/*
+ * Filtered link-prediction ranks — replaces the per-batch body of
+ * KGEModel.test_step (model.py:383-418) with TestDataset's filter semantics
+ * (dataloader.py:134-154).
+ *   queries [nq,3] (h,r,t); mode KGE_HEAD_BATCH ranks the head, KGE_TAIL_BATCH the tail.
+ *   filter CSR: for query q the ids filt_ids[filt_off[q] .. filt_off[q+1]) are the
+ *   candidates (other than the true one) that form a true triple in
+ *   all_true_triples; the reference gives them bias -1 and the true id
+ *   (dataloader.py:138-144), so they never outrank the positive.
+ *   ranks_out [nq] int64: 1 + #{unfiltered e != true : score_e > score_true}.
+ *   ties_out  [nq] int32 (nullable): #{unfiltered e != true : score_e == score_true}
+ *   (the reference's argsort is not stable; a tie may land either side).
+ */
+size_t kge_rank_workspace_bytes(const kge_model_desc *m, int64_t nq);
+int kge_rank_filtered(const kge_model_desc *m, int32_t mode, const int64_t *queries, int64_t nq,
+                      const int64_t *filt_off, const int64_t *filt_ids, int64_t *ranks_out,
+                      int32_t *ties_out, void *workspace, size_t workspace_bytes, int32_t *err_flag,
+                      void *stream);
+
+/*
+ * Live stage timing for benchmarks (no reference counterpart): when enabled,
+ * kge_train_step_grads records a hipEvent on its stream before and after each
+ * stage — 0 row pass (fused scoring + loss), 1 occurrence CSR, 2 entity-major
+ * gradient pass, 3 relation pass + loss finalisation.
+ *   command 1: enable and reset; 0: disable and reset;
+ *   command 2: synchronise the recorded events and write the summed
+ *              milliseconds per stage to stage_ms_out[0..3] and the number of
+ *              timed calls to stage_ms_out[4] (n_out >= 5).
+ * Not graph-capturable while enabled.
+ */
+#define KGE_TIMER_STAGES 4
+int kge_stage_timer(int32_t command, float *stage_ms_out, int32_t n_out);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* KGE_HIP_H */

@@ -1,0 +1,100 @@
+"""ctypes binding of the C-ABI in include/kge_hip.h.
+
+The HIP library is the ONLY compute path of this package: if libkge_hip.so is
+missing or a call fails, the error propagates — there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from pathlib import Path
+
+_PKG = Path(__file__).resolve().parent
+LIB_PATH = Path(os.environ.get("KGE_HIP_LIB", _PKG / "libkge_hip.so"))
+
+# enum kge_model_id / kge_mode_id (include/kge_hip.h)
+MODEL_IDS = {"TransE": 0, "DistMult": 1, "ComplEx": 2, "RotatE": 3, "pRotatE": 4}
+MODE_IDS = {"single": 0, "head-batch": 1, "tail-batch": 2}
+DEVERR_INDEX = 1
+ERR_HIP_BASE = 1000
+
+
+class ModelDesc(C.Structure):
+    """struct kge_model_desc."""
+
+    _fields_ = [
+        ("model", C.c_int32),
+        ("entity_dim", C.c_int32),
+        ("relation_dim", C.c_int32),
+        ("reserved", C.c_int32),
+        ("nentity", C.c_int64),
+        ("nrelation", C.c_int64),
+        ("gamma", C.c_float),
+        ("phase_divisor", C.c_float),
+        ("phase_divisor_p", C.c_float),
+        ("reserved_f", C.c_float),
+        ("entity_embedding", C.c_void_p),
+        ("relation_embedding", C.c_void_p),
+        ("modulus", C.c_void_p),
+    ]
+
+
+_P = C.c_void_p
+_I32 = C.c_int32
+_I64 = C.c_int64
+_F = C.c_float
+_SZ = C.c_size_t
+_DESC = C.POINTER(ModelDesc)
+
+# name -> (restype, argtypes); this table is also the symbol list the
+# "library loads and exports every symbol" test checks against include/kge_hip.h.
+SIGNATURES = {
+    "kge_version": (C.c_char_p, []),
+    "kge_status_string": (C.c_char_p, [C.c_int]),
+    "kge_score": (C.c_int, [_DESC, _I32, _P, _P, _I64, _I64, _P, _P, _P]),
+    "kge_backward_workspace_bytes": (_SZ, [_DESC, _I32, _I64, _I64]),
+    "kge_score_backward": (C.c_int, [_DESC, _I32, _P, _P, _I64, _I64, _P, _P, _P, _P, _P, _SZ, _P, _P]),
+    "kge_train_workspace_bytes": (_SZ, [_DESC, _I64, _I64]),
+    "kge_train_step_grads": (
+        C.c_int,
+        [_DESC, _I32, _P, _P, _I64, _I64, _P, _P, _I32, _I64, _I32, _F, _F, _P, _P, _P, _P, _P, _SZ, _P, _P],
+    ),
+    "kge_weight_sum": (C.c_int, [_P, _I64, _P, _P]),
+    "kge_adam_step": (C.c_int, [_P, _P, _P, _P, _I64, _F, _F, _F, _F, _F, _P]),
+    "kge_rank_workspace_bytes": (_SZ, [_DESC, _I64]),
+    "kge_rank_filtered": (C.c_int, [_DESC, _I32, _P, _I64, _P, _P, _P, _P, _P, _SZ, _P, _P]),
+    "kge_stage_timer": (C.c_int, [_I32, _P, _I32]),
+}
+
+_lib = None
+
+
+class KGEHipError(RuntimeError):
+    pass
+
+
+def load() -> C.CDLL:
+    """Load libkge_hip.so (built by knowledgegraphembedding_amd.build) or raise."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not LIB_PATH.exists():
+        raise KGEHipError(
+            f"{LIB_PATH} is missing: build it with `python -m knowledgegraphembedding_amd.build` "
+            "(hipcc, gfx950). knowledgegraphembedding_amd has no CPU fallback."
+        )
+    lib = C.CDLL(str(LIB_PATH))
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def check(status: int, what: str) -> None:
+    if status != 0:
+        msg = load().kge_status_string(status).decode()
+        if status == 1:
+            raise ValueError(f"{what}: {msg}")
+        raise KGEHipError(f"{what} failed with status {status}: {msg}")

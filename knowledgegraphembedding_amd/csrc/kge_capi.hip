@@ -1,0 +1,429 @@
+// kge_capi.hip — the extern "C" boundary declared in include/kge_hip.h.
+// Host-side argument checks, workspace carving and launch sequencing; no
+// allocation, no synchronisation (graph-capturable).
+#include <string.h>
+
+#include <vector>
+
+#include "kge_common.h"
+
+namespace kge {
+namespace {
+
+struct Geom {
+  int vec, ns;
+  RowGeom eg;
+  bool cplx;
+};
+
+const ModelOps& ops_for(int model) {
+  static const ModelOps tbl[5] = {model_ops_transe(), model_ops_distmult(), model_ops_complex(),
+                                  model_ops_rotate(), model_ops_protate()};
+  return tbl[model];
+}
+
+int hip_status(hipError_t e) { return e == hipSuccess ? KGE_OK : (KGE_ERR_HIP_BASE + (int)e); }
+int launch_status(int e) { return e == 0 ? KGE_OK : (e < 0 ? KGE_ERR_DIM : KGE_ERR_HIP_BASE + e); }
+
+bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
+
+// model.py:63-70 plus the broadcast rules of the plug-ins.
+int check_model(const kge_model_desc* m, Geom* g) {
+  if (!m) return KGE_ERR_ARG;
+  if (m->model < KGE_TRANSE || m->model > KGE_PROTATE) return KGE_ERR_MODEL;
+  if (!m->entity_embedding || !m->relation_embedding) return KGE_ERR_ARG;
+  if (m->nentity <= 0 || m->nrelation <= 0 || m->entity_dim <= 0 || m->relation_dim <= 0) return KGE_ERR_ARG;
+  if (m->nentity >= (int64_t)1 << 31 || m->nrelation >= (int64_t)1 << 30) return KGE_ERR_DIM;
+  const int Le = m->entity_dim, Lr = m->relation_dim;
+  g->cplx = (m->model == KGE_COMPLEX || m->model == KGE_ROTATE);
+  int span;
+  if (m->model == KGE_ROTATE) {
+    if (Le != 2 * Lr) return KGE_ERR_SHAPE;  // RotatE: -de, not -dr
+    span = Lr;
+  } else if (m->model == KGE_COMPLEX) {
+    if (Le != Lr || (Le & 1)) return KGE_ERR_SHAPE;  // ComplEx: -de and -dr
+    span = Le / 2;
+  } else {
+    if (Le != Lr) return KGE_ERR_SHAPE;
+    span = Le;
+  }
+  if (m->model == KGE_PROTATE && !m->modulus) return KGE_ERR_ARG;
+  const bool v4 = (span % 4 == 0) && aligned16(m->entity_embedding) && aligned16(m->relation_embedding);
+  g->vec = v4 ? 4 : 1;
+  const int S = span / g->vec;
+  int ns = 1;
+  while (64 * ns < S) ns *= 2;
+  if (ns > 8) return KGE_ERR_DIM;
+  g->ns = ns;
+  g->eg.S = S;
+  g->eg.half = g->cplx ? span : 0;
+  return KGE_OK;
+}
+
+Consts consts_of(const kge_model_desc* m) {
+  Consts c;
+  c.gamma = m->gamma;
+  c.kappa = m->phase_divisor;
+  c.kappa_p = m->phase_divisor_p;
+  c.modulus = 0.f;
+  return c;
+}
+
+struct Carver {
+  char* base;
+  size_t off = 0;
+  explicit Carver(void* p) : base((char*)p) {}
+  template <typename T>
+  T* take(size_t count) {
+    off = (off + 255) & ~(size_t)255;
+    T* p = base ? (T*)(base + off) : nullptr;
+    off += count * sizeof(T);
+    return p;
+  }
+};
+
+struct GradWs {
+  float *g, *q, *ent_contrib, *rel_contrib, *row_stats, *reg_partial, *wsum;
+  int32_t *keys, *cnt, *off, *tmp, *occ;
+};
+
+GradWs carve_grad(void* ws, const kge_model_desc* m, int64_t B, int64_t n, size_t* bytes) {
+  Carver c(ws);
+  GradWs w;
+  const int64_t Bn = B * n, N = Bn + 3 * B, nb = m->nentity + m->nrelation;
+  w.g = c.take<float>(Bn);
+  w.q = c.take<float>(B * (int64_t)m->entity_dim);
+  w.ent_contrib = c.take<float>(2 * B * (int64_t)m->entity_dim);
+  w.rel_contrib = c.take<float>(B * (int64_t)m->relation_dim);
+  w.row_stats = c.take<float>(B * 4);
+  w.reg_partial = c.take<float>(nb);
+  w.wsum = c.take<float>(4);
+  w.keys = c.take<int32_t>(N);
+  w.cnt = c.take<int32_t>(nb);
+  w.off = c.take<int32_t>(nb + 1);
+  w.tmp = c.take<int32_t>(N);
+  w.occ = c.take<int32_t>(N);
+  *bytes = c.off + 256;
+  return w;
+}
+
+hipStream_t as_stream(void* s) { return (hipStream_t)s; }
+
+// ---- stage timer (bench instrumentation; see kge_stage_timer in the header)
+struct StageTimer {
+  bool on = false;
+  std::vector<hipEvent_t> ev;  // (KGE_TIMER_STAGES + 1) events per timed call
+  size_t used = 0;             // events recorded so far
+  hipEvent_t next(hipStream_t) {
+    if (used == ev.size()) {
+      hipEvent_t e;
+      if (hipEventCreate(&e) != hipSuccess) return nullptr;
+      ev.push_back(e);
+    }
+    return ev[used++];
+  }
+  void mark(hipStream_t s) {
+    if (!on) return;
+    hipEvent_t e = next(s);
+    if (e) hipEventRecord(e, s);
+  }
+};
+StageTimer g_timer;
+
+// Shared body of backward and train: row pass → CSR → entity pass → relation pass → finalise.
+int run_grad(const kge_model_desc* m, const Geom& geo, int mode, const int64_t* pos, const int64_t* neg,
+             int64_t neg_stride, int64_t B, int64_t n, RowArgs ra, GradWs w, float* grad_entity,
+             float* grad_relation, float* grad_modulus, float reg, FinArgs fa, int32_t* err, hipStream_t s) {
+  const ModelOps& op = ops_for(m->model);
+  const Consts c = consts_of(m);
+  const int Le = m->entity_dim, Lr = m->relation_dim;
+  const size_t lds = sizeof(float) * (4 * (size_t)Le + (size_t)ra.n_lds + 32);
+  if (lds > 64 * 1024) return KGE_ERR_DIM;
+  const bool timed = g_timer.on && ra.op == ROW_TRAIN;
+  if (timed) g_timer.mark(s);
+  int st = launch_status(op.row(mode, geo.vec, geo.ns, ra, lds, s));
+  if (st) return st;
+  if (timed) g_timer.mark(s);
+
+  CsrArgs ca;
+  ca.pos = pos; ca.neg = neg; ca.neg_stride = neg_stride;
+  ca.B = B; ca.n = n; ca.Bn = B * n; ca.E = m->nentity; ca.R = m->nrelation;
+  ca.keys = w.keys; ca.cnt = w.cnt; ca.off = w.off; ca.tmp = w.tmp; ca.occ = w.occ; ca.err = err;
+  st = launch_status(launch_csr(ca, s));
+  if (st) return st;
+  if (timed) g_timer.mark(s);
+
+  EntArgs ea;
+  ea.ent = m->entity_embedding; ea.modulus = m->modulus; ea.E = m->nentity; ea.Le = Le; ea.eg = geo.eg;
+  ea.c = c; ea.off = w.off; ea.occ = w.occ; ea.Bn = B * n; ea.n = n;
+  ea.g = (ra.op == ROW_TRAIN) ? w.g : ra.g_in;
+  ea.q = w.q; ea.ent_contrib = w.ent_contrib; ea.reg3 = 3.f * reg; ea.reg_partial = w.reg_partial;
+  ea.grad_ent = grad_entity;
+  st = launch_status(op.entity(mode, geo.vec, geo.ns, ea, s));
+  if (st) return st;
+  if (timed) g_timer.mark(s);
+
+  RelArgs rl;
+  rl.rel = m->relation_embedding; rl.R = m->nrelation; rl.E = m->nentity; rl.B = B; rl.Bn = B * n; rl.Lr = Lr;
+  rl.off = w.off; rl.occ = w.occ; rl.rel_contrib = w.rel_contrib; rl.reg3 = 3.f * reg;
+  rl.reg_partial = w.reg_partial + m->nentity; rl.grad_rel = grad_relation;
+  st = launch_status(launch_rel_rows(rl, s));
+  if (st) return st;
+
+  fa.row_stats = w.row_stats;
+  fa.reg_partial = (reg != 0.f) ? w.reg_partial : nullptr;
+  fa.nreg = m->nentity + m->nrelation;
+  fa.regularization = reg;
+  fa.grad_modulus = grad_modulus;
+  if (fa.losses || grad_modulus) {
+    st = launch_status(launch_finalize(fa, s));
+    if (st) return st;
+  }
+  if (timed) g_timer.mark(s);
+  return KGE_OK;
+}
+
+RowArgs row_args(const kge_model_desc* m, const Geom& geo, const int64_t* pos, const int64_t* neg, int64_t ns,
+                 int64_t B, int64_t n, GradWs w, int32_t* err) {
+  RowArgs ra;
+  memset(&ra, 0, sizeof(ra));
+  ra.ent = m->entity_embedding; ra.rel = m->relation_embedding; ra.modulus = m->modulus;
+  ra.pos = pos; ra.neg = neg; ra.neg_stride = ns;
+  ra.B = B; ra.n = n; ra.E = m->nentity; ra.R = m->nrelation;
+  ra.Le = m->entity_dim; ra.Lr = m->relation_dim; ra.eg = geo.eg; ra.c = consts_of(m);
+  ra.g_out = w.g; ra.q_out = w.q; ra.ent_contrib = w.ent_contrib; ra.rel_contrib = w.rel_contrib;
+  ra.row_stats = w.row_stats; ra.err = err;
+  return ra;
+}
+
+}  // namespace
+}  // namespace kge
+
+using namespace kge;
+
+extern "C" {
+
+const char* kge_version(void) { return "knowledgegraphembedding_amd 0.1 gfx950"; }
+
+const char* kge_status_string(int status) {
+  switch (status) {
+    case KGE_OK: return "ok";
+    case KGE_ERR_MODEL: return "model not supported";
+    case KGE_ERR_MODE: return "mode not supported";
+    case KGE_ERR_SHAPE: return "entity/relation dims inconsistent with the model";
+    case KGE_ERR_ARG: return "invalid argument";
+    case KGE_ERR_WORKSPACE: return "workspace too small";
+    case KGE_ERR_DIM: return "row length / negative count outside the compiled kernel range";
+    default:
+      if (status >= KGE_ERR_HIP_BASE) return hipGetErrorString((hipError_t)(status - KGE_ERR_HIP_BASE));
+      return "unknown";
+  }
+}
+
+int kge_score(const kge_model_desc* m, int32_t mode, const int64_t* pos, const int64_t* neg, int64_t batch,
+              int64_t nneg, float* out, int32_t* err_flag, void* stream) {
+  Geom geo;
+  int st = check_model(m, &geo);
+  if (st) return st;
+  if (mode != KGE_SINGLE && mode != KGE_HEAD_BATCH && mode != KGE_TAIL_BATCH) return KGE_ERR_MODE;
+  if (!pos || !out || !err_flag || batch < 0 || nneg < 1) return KGE_ERR_ARG;
+  if (batch == 0) return KGE_OK;
+  ScoreArgs a;
+  a.ent = m->entity_embedding; a.rel = m->relation_embedding; a.modulus = m->modulus;
+  a.pos = pos;
+  if (mode == KGE_SINGLE) {
+    if (nneg != 1) return KGE_ERR_ARG;
+    a.neg = pos + 2;  // 'single' scores (h, r, t) with the tail-batch formulas, t in place of a negative
+    a.neg_stride = 3;
+  } else {
+    if (!neg) return KGE_ERR_ARG;
+    a.neg = neg;
+    a.neg_stride = nneg;
+  }
+  a.B = batch; a.n = nneg; a.E = m->nentity; a.R = m->nrelation;
+  a.Le = m->entity_dim; a.Lr = m->relation_dim; a.eg = geo.eg; a.c = consts_of(m);
+  a.jpw = nneg < 16 ? nneg : 16;
+  a.out = out; a.err = err_flag;
+  const int64_t units = batch * ((nneg + a.jpw - 1) / a.jpw);
+  const int kmode = (mode == KGE_HEAD_BATCH) ? HEAD_BATCH : TAIL_BATCH;
+  return launch_status(ops_for(m->model).score(kmode, geo.vec, geo.ns, a, units, as_stream(stream)));
+}
+
+size_t kge_backward_workspace_bytes(const kge_model_desc* m, int32_t mode, int64_t batch, int64_t nneg) {
+  (void)mode;
+  size_t b = 0;
+  carve_grad(nullptr, m, batch, nneg, &b);
+  return b;
+}
+
+int kge_score_backward(const kge_model_desc* m, int32_t mode, const int64_t* pos, const int64_t* neg, int64_t batch,
+                       int64_t nneg, const float* grad_scores, float* grad_entity, float* grad_relation,
+                       float* grad_modulus, void* workspace, size_t workspace_bytes, int32_t* err_flag,
+                       void* stream) {
+  Geom geo;
+  int st = check_model(m, &geo);
+  if (st) return st;
+  if (mode != KGE_SINGLE && mode != KGE_HEAD_BATCH && mode != KGE_TAIL_BATCH) return KGE_ERR_MODE;
+  if (!pos || !grad_scores || !grad_entity || !grad_relation || !err_flag || batch < 1 || nneg < 1)
+    return KGE_ERR_ARG;
+  const int64_t* negp = neg;
+  int64_t ns = nneg;
+  if (mode == KGE_SINGLE) {
+    if (nneg != 1) return KGE_ERR_ARG;
+    negp = pos + 2;
+    ns = 3;
+  } else if (!neg) {
+    return KGE_ERR_ARG;
+  }
+  size_t need = 0;
+  GradWs w = carve_grad(workspace, m, batch, nneg, &need);
+  if (!workspace || workspace_bytes < need) return KGE_ERR_WORKSPACE;
+  RowArgs ra = row_args(m, geo, pos, negp, ns, batch, nneg, w, err_flag);
+  ra.op = ROW_GIVEN;
+  ra.g_in = grad_scores;
+  ra.n_lds = 0;
+  FinArgs fa;
+  memset(&fa, 0, sizeof(fa));
+  fa.B = batch;
+  fa.uni_weight = 1;
+  fa.uni_n = 1.f;
+  fa.losses = nullptr;
+  const int kmode = (mode == KGE_HEAD_BATCH) ? HEAD_BATCH : TAIL_BATCH;
+  return run_grad(m, geo, kmode, pos, negp, ns, batch, nneg, ra, w, grad_entity, grad_relation,
+                  m->model == KGE_PROTATE ? grad_modulus : nullptr, 0.f, fa, err_flag, as_stream(stream));
+}
+
+size_t kge_train_workspace_bytes(const kge_model_desc* m, int64_t batch, int64_t nneg) {
+  size_t b = 0;
+  carve_grad(nullptr, m, batch, nneg, &b);
+  return b;
+}
+
+int kge_train_step_grads(const kge_model_desc* m, int32_t mode, const int64_t* pos, const int64_t* neg,
+                         int64_t batch, int64_t nneg, const float* subsampling_weight, const float* weight_sum,
+                         int32_t uni_weight, int64_t uni_batch, int32_t adversarial,
+                         float adversarial_temperature, float regularization, float* grad_entity,
+                         float* grad_relation, float* grad_modulus, float* losses_out, void* workspace,
+                         size_t workspace_bytes, int32_t* err_flag, void* stream) {
+  Geom geo;
+  int st = check_model(m, &geo);
+  if (st) return st;
+  if (mode != KGE_HEAD_BATCH && mode != KGE_TAIL_BATCH) return KGE_ERR_MODE;
+  if (!pos || !neg || !grad_entity || !grad_relation || !err_flag || !losses_out || batch < 1 || nneg < 1)
+    return KGE_ERR_ARG;
+  if (!uni_weight && !subsampling_weight) return KGE_ERR_ARG;
+  if (m->model == KGE_PROTATE && !grad_modulus) return KGE_ERR_ARG;
+  size_t need = 0;
+  GradWs w = carve_grad(workspace, m, batch, nneg, &need);
+  if (!workspace || workspace_bytes < need) return KGE_ERR_WORKSPACE;
+  hipStream_t s = as_stream(stream);
+  const float* wsum = weight_sum;
+  if (!uni_weight && !wsum) {
+    st = launch_status(launch_weight_sum(subsampling_weight, batch, w.wsum, s));
+    if (st) return st;
+    wsum = w.wsum;
+  }
+  const int64_t ub = uni_batch > 0 ? uni_batch : batch;
+  RowArgs ra = row_args(m, geo, pos, neg, nneg, batch, nneg, w, err_flag);
+  ra.op = ROW_TRAIN;
+  ra.adversarial = adversarial ? 1 : 0;
+  ra.adv_T = adversarial_temperature;
+  ra.uni_weight = uni_weight ? 1 : 0;
+  ra.uni_inv = 1.f / (float)ub;
+  ra.sub_w = subsampling_weight;
+  ra.w_sum = wsum;
+  ra.n_lds = (int)nneg;
+  if (nneg > 8192) return KGE_ERR_DIM;
+  FinArgs fa;
+  memset(&fa, 0, sizeof(fa));
+  fa.sub_w = subsampling_weight;
+  fa.w_sum = wsum;
+  fa.B = batch;
+  fa.uni_weight = uni_weight ? 1 : 0;
+  fa.uni_n = (float)ub;
+  fa.losses = losses_out;
+  return run_grad(m, geo, mode, pos, neg, nneg, batch, nneg, ra, w, grad_entity, grad_relation,
+                  m->model == KGE_PROTATE ? grad_modulus : nullptr, regularization, fa, err_flag, s);
+}
+
+int kge_weight_sum(const float* w, int64_t n, float* out, void* stream) {
+  if (!w || !out || n < 0) return KGE_ERR_ARG;
+  return launch_status(launch_weight_sum(w, n, out, as_stream(stream)));
+}
+
+int kge_adam_step(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t numel, float beta1,
+                  float beta2, float eps, float step_size, float bias_correction2_sqrt, void* stream) {
+  if (!param || !grad || !exp_avg || !exp_avg_sq || numel < 0) return KGE_ERR_ARG;
+  if (numel == 0) return KGE_OK;
+  if (!aligned16(param) || !aligned16(grad) || !aligned16(exp_avg) || !aligned16(exp_avg_sq)) return KGE_ERR_ARG;
+  return launch_status(launch_adam(param, grad, exp_avg, exp_avg_sq, numel, beta1, beta2, eps, step_size,
+                                   bias_correction2_sqrt, as_stream(stream)));
+}
+
+size_t kge_rank_workspace_bytes(const kge_model_desc* m, int64_t nq) {
+  Carver c(nullptr);
+  c.take<float>(nq * (int64_t)m->entity_dim);
+  c.take<float>(nq);
+  c.take<int64_t>(nq);
+  c.take<int32_t>(nq);
+  c.take<int32_t>(nq);
+  return c.off + 256;
+}
+
+int kge_rank_filtered(const kge_model_desc* m, int32_t mode, const int64_t* queries, int64_t nq,
+                      const int64_t* filt_off, const int64_t* filt_ids, int64_t* ranks_out, int32_t* ties_out,
+                      void* workspace, size_t workspace_bytes, int32_t* err_flag, void* stream) {
+  Geom geo;
+  int st = check_model(m, &geo);
+  if (st) return st;
+  if (mode != KGE_HEAD_BATCH && mode != KGE_TAIL_BATCH) return KGE_ERR_MODE;
+  if (!queries || !filt_off || !ranks_out || !err_flag || nq < 0) return KGE_ERR_ARG;
+  if (nq == 0) return KGE_OK;
+  if (workspace_bytes < kge_rank_workspace_bytes(m, nq) || !workspace) return KGE_ERR_WORKSPACE;
+  Carver c(workspace);
+  RankArgs a;
+  a.ent = m->entity_embedding; a.rel = m->relation_embedding; a.modulus = m->modulus;
+  a.queries = queries; a.nq = nq; a.E = m->nentity; a.R = m->nrelation;
+  a.Le = m->entity_dim; a.Lr = m->relation_dim; a.eg = geo.eg; a.c = consts_of(m);
+  a.filt_off = filt_off; a.filt_ids = filt_ids;
+  a.cpw = 64;
+  a.q = c.take<float>(nq * (int64_t)m->entity_dim);
+  a.s_true = c.take<float>(nq);
+  a.true_id = c.take<int64_t>(nq);
+  a.gt = c.take<int32_t>(nq);
+  a.eq = c.take<int32_t>(nq);
+  a.ranks = ranks_out; a.ties = ties_out; a.err = err_flag;
+  hipStream_t s = as_stream(stream);
+  hipError_t e = hipMemsetAsync(a.gt, 0, sizeof(int32_t) * nq, s);
+  if (e != hipSuccess) return hip_status(e);
+  e = hipMemsetAsync(a.eq, 0, sizeof(int32_t) * nq, s);
+  if (e != hipSuccess) return hip_status(e);
+  return launch_status(ops_for(m->model).rank(mode, geo.vec, geo.ns, a, s));
+}
+
+int kge_stage_timer(int32_t command, float* stage_ms_out, int32_t n_out) {
+  constexpr int NS_ = KGE_TIMER_STAGES + 1;
+  if (command == 0 || command == 1) {
+    g_timer.on = (command == 1);
+    g_timer.used = 0;
+    return KGE_OK;
+  }
+  if (command != 2 || !stage_ms_out || n_out < NS_) return KGE_ERR_ARG;
+  for (int k = 0; k < NS_; ++k) stage_ms_out[k] = 0.f;
+  const size_t calls = g_timer.used / NS_;
+  for (size_t c = 0; c < calls; ++c) {
+    hipEvent_t* e = &g_timer.ev[c * NS_];
+    hipError_t err = hipEventSynchronize(e[NS_ - 1]);
+    if (err != hipSuccess) return hip_status(err);
+    for (int k = 0; k < KGE_TIMER_STAGES; ++k) {
+      float ms = 0.f;
+      err = hipEventElapsedTime(&ms, e[k], e[k + 1]);
+      if (err != hipSuccess) return hip_status(err);
+      stage_ms_out[k] += ms;
+    }
+  }
+  stage_ms_out[KGE_TIMER_STAGES] = (float)calls;
+  return KGE_OK;
+}
+
+}  // extern "C"

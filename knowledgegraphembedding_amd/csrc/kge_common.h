@@ -1,0 +1,53 @@
+// kge_common.h — argument blocks and launchers of the model-independent kernels.
+#pragma once
+#include "kge_internal.h"
+
+namespace kge {
+
+struct CsrArgs {
+  const int64_t* pos;
+  const int64_t* neg;
+  int64_t neg_stride;
+  int64_t B, n, Bn, E, R;
+  int32_t* keys;  // [Bn + 3B]
+  int32_t* cnt;   // [E + R]
+  int32_t* off;   // [E + R + 1]
+  int32_t* tmp;   // [Bn + 3B]
+  int32_t* occ;   // [Bn + 3B]
+  int32_t* err;
+};
+
+struct RelArgs {
+  const float* rel;
+  int64_t R, E, B, Bn;
+  int Lr;
+  const int32_t* off;
+  const int32_t* occ;
+  const float* rel_contrib;  // [B, Lr]
+  float reg3;
+  float* reg_partial;        // [R]
+  float* grad_rel;
+};
+
+struct FinArgs {
+  const float* row_stats;    // [B, 4]
+  const float* sub_w;        // nullable
+  const float* w_sum;        // nullable → Σ of sub_w
+  int64_t B;
+  int uni_weight;
+  float uni_n;               // global batch size (uni_weight means)
+  const float* reg_partial;  // [nreg] or null
+  int64_t nreg;
+  float regularization;
+  float* losses;             // [4]
+  float* grad_modulus;       // nullable
+};
+
+int launch_csr(const CsrArgs& a, hipStream_t s);
+int launch_rel_rows(const RelArgs& a, hipStream_t s);
+int launch_finalize(const FinArgs& a, hipStream_t s);
+int launch_weight_sum(const float* w, int64_t n, float* out, hipStream_t s);
+int launch_adam(float* p, const float* g, float* m, float* v, int64_t n, float b1, float b2, float eps,
+                float step_size, float bc2s, hipStream_t s);
+
+}  // namespace kge

@@ -1,0 +1,289 @@
+// kge_common.hip — model-independent kernels: occurrence CSR (deterministic
+// counting sort), relation-gradient row sums, loss finalisation, Σw and Adam.
+#include "kge_common.h"
+
+namespace kge {
+
+// -------------------------------------------------------------- CSR build
+// Keys of one training/backward call, in id order:
+//   [0, Bn)            negative occurrence (i, j): entity neg[i*ns + j]
+//   [Bn, Bn+2B)        row slot s: entity pos[(s/2)*3 + (s&1 ? 2 : 0)]
+//   [Bn+2B, Bn+3B)     relation of row i: bucket E + pos[i*3 + 1]
+__global__ __launch_bounds__(256) void k_csr_hist(CsrArgs a) {
+  const int64_t N = a.Bn + 3 * a.B;
+  for (int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x; k < N; k += (int64_t)gridDim.x * 256) {
+    int64_t key;
+    if (k < a.Bn) {
+      const int64_t i = k / a.n, j = k - i * a.n;
+      key = a.neg[i * a.neg_stride + j];
+      if (key < 0 || key >= a.E) key = -1;
+    } else if (k < a.Bn + 2 * a.B) {
+      const int64_t s = k - a.Bn;
+      key = a.pos[(s >> 1) * 3 + ((s & 1) ? 2 : 0)];
+      if (key < 0 || key >= a.E) key = -1;
+    } else {
+      const int64_t i = k - a.Bn - 2 * a.B;
+      key = a.pos[i * 3 + 1];
+      key = (key < 0 || key >= a.R) ? -1 : (a.E + key);
+    }
+    if (key < 0) {
+      atomicOr(a.err, KGE_DEVERR_INDEX);
+      a.keys[k] = -1;
+      continue;
+    }
+    a.keys[k] = (int32_t)key;
+    atomicAdd(&a.cnt[key], 1);
+  }
+}
+
+// Exclusive scan of cnt[0..nb) into off[0..nb]; one workgroup of 1024 threads.
+__global__ __launch_bounds__(1024) void k_csr_scan(const int32_t* __restrict__ cnt, int32_t* __restrict__ off,
+                                                   int64_t nb) {
+  __shared__ int32_t part[1024];
+  const int tid = threadIdx.x;
+  const int64_t per = (nb + 1023) / 1024;
+  const int64_t b0 = tid * per, b1 = (b0 + per < nb) ? (b0 + per) : nb;
+  int32_t s = 0;
+  for (int64_t k = b0; k < b1; ++k) s += cnt[k];
+  part[tid] = s;
+  __syncthreads();
+  for (int o = 1; o < 1024; o <<= 1) {
+    const int32_t v = (tid >= o) ? part[tid - o] : 0;
+    __syncthreads();
+    part[tid] += v;
+    __syncthreads();
+  }
+  int32_t run = part[tid] - s;  // exclusive prefix of this thread's chunk
+  for (int64_t k = b0; k < b1; ++k) {
+    off[k] = run;
+    run += cnt[k];
+  }
+  if (tid == 1023) off[nb] = part[1023];
+}
+
+// Unordered fill: slot = off[key] + (--cnt[key]).
+__global__ __launch_bounds__(256) void k_csr_fill(CsrArgs a) {
+  const int64_t N = a.Bn + 3 * a.B;
+  for (int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x; k < N; k += (int64_t)gridDim.x * 256) {
+    const int32_t key = a.keys[k];
+    if (key < 0) continue;
+    const int32_t p = atomicSub(&a.cnt[key], 1) - 1;
+    a.tmp[a.off[key] + p] = (int32_t)k;
+  }
+}
+
+// Deterministic order: each id's final slot is its rank among the ids of its
+// bucket (ids are unique), so buckets come out ascending whatever order the
+// atomics filled them in.
+__global__ __launch_bounds__(256) void k_csr_rank(CsrArgs a) {
+  const int64_t N = a.Bn + 3 * a.B;
+  for (int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x; k < N; k += (int64_t)gridDim.x * 256) {
+    const int32_t key = a.keys[k];
+    if (key < 0) continue;
+    const int32_t b0 = a.off[key], b1 = a.off[key + 1];
+    int32_t r = 0;
+    for (int32_t p = b0; p < b1; ++p) r += (a.tmp[p] < (int32_t)k);
+    a.occ[b0 + r] = (int32_t)k;
+  }
+}
+
+// -------------------------------------------------- relation gradient rows
+// One wave per relation row: Σ of the rows' relation contributions in id
+// order (+ 3λ r|r|), written densely.
+__global__ __launch_bounds__(256) void k_rel_rows(RelArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int64_t rr = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (rr >= a.R) return;
+  const int32_t b0 = a.off[a.E + rr], b1 = a.off[a.E + rr + 1];
+  const float* row = a.rel + rr * a.Lr;
+  float* out = a.grad_rel + rr * a.Lr;
+  float part = 0.f;
+  for (int k0 = 0; k0 < a.Lr; k0 += 64 * 4) {
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int32_t p = b0; p < b1; ++p) {
+      const int64_t i = a.occ[p] - a.Bn - 2 * a.B;
+      const float* src = a.rel_contrib + i * a.Lr;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int k = k0 + u * 64 + lane;
+        if (k < a.Lr) acc[u] += src[k];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int k = k0 + u * 64 + lane;
+      if (k < a.Lr) {
+        float v = acc[u];
+        if (a.reg3 != 0.f) {
+          const float x = row[k];
+          v += a.reg3 * (x * fabsf(x));
+          part += fabsf(x) * x * x;
+        }
+        out[k] = v;
+      }
+    }
+  }
+  if (a.reg3 != 0.f) {
+    part = wave_sum(part);
+    if (lane == 0) a.reg_partial[rr] = part;
+  }
+}
+
+// ------------------------------------------------------------ finalise
+// Loss scalars (model.py:279-297) and d/dmodulus.  One workgroup, fixed
+// reduction order.
+__global__ __launch_bounds__(1024) void k_finalize(FinArgs a) {
+  __shared__ float red[6][1024];
+  const int tid = threadIdx.x;
+  float sw = 0.f, swp = 0.f, swn = 0.f, sp = 0.f, sn = 0.f, mg = 0.f;
+  for (int64_t i = tid; i < a.B; i += 1024) {
+    const float* st = a.row_stats + i * 4;
+    const float w = a.sub_w ? a.sub_w[i] : 1.f;
+    sw += w;
+    swp += w * st[0];
+    swn += w * st[1];
+    sp += st[0];
+    sn += st[1];
+    mg += st[2];
+  }
+  red[0][tid] = sw; red[1][tid] = swp; red[2][tid] = swn;
+  red[3][tid] = sp; red[4][tid] = sn; red[5][tid] = mg;
+  __syncthreads();
+  for (int o = 512; o > 0; o >>= 1) {
+    if (tid < o)
+      for (int u = 0; u < 6; ++u) red[u][tid] += red[u][tid + o];
+    __syncthreads();
+  }
+  float tot[6];
+#pragma unroll
+  for (int u = 0; u < 6; ++u) tot[u] = red[u][0];
+  float reg = 0.f;
+  if (a.reg_partial && a.nreg > 0) {
+    float s = 0.f;
+    for (int64_t k = tid; k < a.nreg; k += 1024) s += a.reg_partial[k];
+    __syncthreads();
+    red[0][tid] = s;
+    __syncthreads();
+    for (int o = 512; o > 0; o >>= 1) {
+      if (tid < o) red[0][tid] += red[0][tid + o];
+      __syncthreads();
+    }
+    reg = a.regularization * red[0][0];
+  }
+  if (tid == 0) {
+    float pos_loss, neg_loss;
+    if (a.uni_weight) {
+      // - score.mean(): sum / batch  (model.py:282-283)
+      pos_loss = -(tot[3] / a.uni_n);
+      neg_loss = -(tot[4] / a.uni_n);
+    } else {
+      // - (w * score).sum() / w.sum()  (model.py:285-286)
+      const float wsum = a.w_sum ? a.w_sum[0] : tot[0];
+      pos_loss = -(tot[1] / wsum);
+      neg_loss = -(tot[2] / wsum);
+    }
+    float loss = (pos_loss + neg_loss) / 2.f;
+    loss = loss + reg;
+    if (a.losses) {
+      a.losses[0] = pos_loss;
+      a.losses[1] = neg_loss;
+      a.losses[2] = loss;
+      a.losses[3] = reg;
+    }
+    if (a.grad_modulus) a.grad_modulus[0] = tot[5];
+  }
+}
+
+__global__ __launch_bounds__(1024) void k_weight_sum(const float* __restrict__ w, int64_t n, float* out) {
+  __shared__ float red[1024];
+  const int tid = threadIdx.x;
+  float s = 0.f;
+  for (int64_t i = tid; i < n; i += 1024) s += w[i];
+  red[tid] = s;
+  __syncthreads();
+  for (int o = 512; o > 0; o >>= 1) {
+    if (tid < o) red[tid] += red[tid + o];
+    __syncthreads();
+  }
+  if (tid == 0) out[0] = red[0];
+}
+
+// ------------------------------------------------------------------ Adam
+// torch.optim.Adam single-tensor math (torch/optim/adam.py, non-capturable):
+//   m.lerp_(g, 1-b1); v.mul_(b2).addcmul_(g, g, 1-b2);
+//   denom = v.sqrt() / bc2_sqrt + eps; p.addcdiv_(m, denom, -step_size)
+__device__ __forceinline__ void adam_elem(float& p, float g, float& m, float& v, float b1, float b2, float eps,
+                                          float step_size, float bc2s) {
+  const float w = 1.f - b1;  // lerp weight < 0.5 → self + w * (end - self)
+  m = m + w * (g - m);
+  v = v * b2 + (1.f - b2) * (g * g);
+  const float denom = sqrtf(v) / bc2s + eps;
+  p = p + (-step_size) * (m / denom);
+}
+
+__global__ __launch_bounds__(256) void k_adam(float* __restrict__ p, const float* __restrict__ g,
+                                              float* __restrict__ m, float* __restrict__ v, int64_t n, float b1,
+                                              float b2, float eps, float step_size, float bc2s) {
+  const int64_t n4 = n / 4;
+  for (int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x; k < n4; k += (int64_t)gridDim.x * 256) {
+    float4 P = reinterpret_cast<float4*>(p)[k];
+    const float4 G = reinterpret_cast<const float4*>(g)[k];
+    float4 Mv = reinterpret_cast<float4*>(m)[k];
+    float4 Vv = reinterpret_cast<float4*>(v)[k];
+    adam_elem(P.x, G.x, Mv.x, Vv.x, b1, b2, eps, step_size, bc2s);
+    adam_elem(P.y, G.y, Mv.y, Vv.y, b1, b2, eps, step_size, bc2s);
+    adam_elem(P.z, G.z, Mv.z, Vv.z, b1, b2, eps, step_size, bc2s);
+    adam_elem(P.w, G.w, Mv.w, Vv.w, b1, b2, eps, step_size, bc2s);
+    reinterpret_cast<float4*>(p)[k] = P;
+    reinterpret_cast<float4*>(m)[k] = Mv;
+    reinterpret_cast<float4*>(v)[k] = Vv;
+  }
+  for (int64_t k = n4 * 4 + (int64_t)blockIdx.x * 256 + threadIdx.x; k < n; k += (int64_t)gridDim.x * 256) {
+    float P = p[k], Mv = m[k], Vv = v[k];
+    adam_elem(P, g[k], Mv, Vv, b1, b2, eps, step_size, bc2s);
+    p[k] = P; m[k] = Mv; v[k] = Vv;
+  }
+}
+
+// ------------------------------------------------------------ launchers
+static inline unsigned grid_for(int64_t n, unsigned cap = 4096) {
+  int64_t g = (n + 255) / 256;
+  if (g < 1) g = 1;
+  return (unsigned)(g < cap ? g : cap);
+}
+
+int launch_csr(const CsrArgs& a, hipStream_t s) {
+  const int64_t nb = a.E + a.R;
+  const int64_t N = a.Bn + 3 * a.B;
+  hipError_t e = hipMemsetAsync(a.cnt, 0, sizeof(int32_t) * nb, s);
+  if (e != hipSuccess) return (int)e;
+  hipLaunchKernelGGL(k_csr_hist, dim3(grid_for(N)), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(k_csr_scan, dim3(1), dim3(1024), 0, s, a.cnt, a.off, nb);
+  hipLaunchKernelGGL(k_csr_fill, dim3(grid_for(N)), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(k_csr_rank, dim3(grid_for(N)), dim3(256), 0, s, a);
+  return (int)hipGetLastError();
+}
+
+int launch_rel_rows(const RelArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(k_rel_rows, dim3((unsigned)((a.R + 3) / 4)), dim3(256), 0, s, a);
+  return (int)hipGetLastError();
+}
+
+int launch_finalize(const FinArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(k_finalize, dim3(1), dim3(1024), 0, s, a);
+  return (int)hipGetLastError();
+}
+
+int launch_weight_sum(const float* w, int64_t n, float* out, hipStream_t s) {
+  hipLaunchKernelGGL(k_weight_sum, dim3(1), dim3(1024), 0, s, w, n, out);
+  return (int)hipGetLastError();
+}
+
+int launch_adam(float* p, const float* g, float* m, float* v, int64_t n, float b1, float b2, float eps,
+                float step_size, float bc2s, hipStream_t s) {
+  hipLaunchKernelGGL(k_adam, dim3(grid_for((n + 3) / 4, 8192)), dim3(256), 0, s, p, g, m, v, n, b1, b2, eps,
+                     step_size, bc2s);
+  return (int)hipGetLastError();
+}
+
+}  // namespace kge

@@ -1,0 +1,382 @@
+// kge_device.h — device-side model math for the MI355X KGE hot path.
+//
+// Row layout in HBM (the reference's nn.Parameter layout, model.py:42-57):
+//   entity   [E, Le] fp32 row-major; complex models (ComplEx, RotatE) keep
+//            re = [0, K), im = [K, 2K) with K = Le/2 (torch.chunk(., 2, dim=2),
+//            model.py:185-187, 204-205).
+//   relation [R, Lr] fp32; RotatE rows are K phases, ComplEx rows re/im halves,
+//            TransE/DistMult/pRotatE rows are plain Le-vectors.
+//
+// A wave (64 lanes) owns a whole row.  The row is cut into SLOTS of VEC
+// consecutive floats (VEC = 4 → one 16-byte load per slot and per half);
+// lane l holds slots l, l+64, l+128, ... (NS slots per lane).  Complex models
+// cut the K complex dims the same way and each slot carries the matching
+// re/im float groups.  Every per-row sum is: lane-local over its slots in
+// ascending order, then a 64-lane xor-butterfly — a fixed order, so a score is
+// bit-identical wherever it is computed (training, forward, ranking).
+//
+// Every score plug-in of model.py:166-249 is written here in the factored form
+//     score(i, j) = finish( Σ_k phi(q_i[k], e_j[k]) )
+// with q_i a per-positive-row vector (the part of the triple the negatives
+// share) and e_j the gathered candidate row:
+//     tail-batch / single: q = f(h, r), e = t       (model.py:126-146, 83-102)
+//     head-batch:          q = f(r, t), e = h       (model.py:104-124)
+// The association of each reference expression is kept (e.g. TransE head-batch
+// is h + (r - t), model.py:168), and the build uses -ffp-contract=off, so the
+// per-element arithmetic rounds like the reference's elementwise ATen ops.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace kge {
+
+enum Model : int { TRANSE = 0, DISTMULT = 1, COMPLEX = 2, ROTATE = 3, PROTATE = 4 };
+enum Mode : int { SINGLE = 0, HEAD_BATCH = 1, TAIL_BATCH = 2 };
+
+template <int M>
+struct Traits {
+  static constexpr bool cplx = (M == COMPLEX || M == ROTATE);
+  // RotatE relation rows carry K phases (one float per complex dim).
+  static constexpr bool rel_phase = (M == ROTATE);
+};
+
+struct Consts {
+  float gamma;
+  float kappa;    // embedding_range / pi     (model.py:209)
+  float kappa_p;  // embedding_range / pi'    (model.py:236-238, pi typo)
+  float modulus;  // pRotatE modulus value, read from the device parameter
+};
+
+// ---------------------------------------------------------------- loads
+template <int VEC>
+__device__ __forceinline__ void ldv(const float* __restrict__ p, float (&x)[VEC]) {
+  if constexpr (VEC == 4) {
+    const float4 v = *reinterpret_cast<const float4*>(p);
+    x[0] = v.x; x[1] = v.y; x[2] = v.z; x[3] = v.w;
+  } else {
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) x[k] = p[k];
+  }
+}
+template <int VEC>
+__device__ __forceinline__ void stv(float* __restrict__ p, const float (&x)[VEC]) {
+  if constexpr (VEC == 4) {
+    *reinterpret_cast<float4*>(p) = make_float4(x[0], x[1], x[2], x[3]);
+  } else {
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) p[k] = x[k];
+  }
+}
+template <int VEC>
+__device__ __forceinline__ void zv(float (&x)[VEC]) {
+#pragma unroll
+  for (int k = 0; k < VEC; ++k) x[k] = 0.f;
+}
+
+// A row as one lane holds it: NS slots, each VEC floats of the real part (a)
+// and, for complex models, VEC floats of the imaginary part (b).
+template <int NS, int VEC, bool CPLX>
+struct Row {
+  float a[NS][VEC];
+  float b[CPLX ? NS : 1][VEC];
+};
+
+struct RowGeom {
+  int S;     // slots per half-row (complex) or per row (real)
+  int half;  // float offset of the imaginary half (complex), 0 otherwise
+};
+
+template <int NS, int VEC, bool CPLX>
+__device__ __forceinline__ void load_row(const float* __restrict__ base, RowGeom g, int lane,
+                                         Row<NS, VEC, CPLX>& r) {
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    const int slot = lane + 64 * s;
+    if (slot < g.S) {
+      ldv<VEC>(base + slot * VEC, r.a[s]);
+      if constexpr (CPLX) ldv<VEC>(base + g.half + slot * VEC, r.b[s]);
+    } else {
+      zv<VEC>(r.a[s]);
+      if constexpr (CPLX) zv<VEC>(r.b[s]);
+    }
+  }
+}
+template <int NS, int VEC, bool CPLX>
+__device__ __forceinline__ void store_row(float* __restrict__ base, RowGeom g, int lane,
+                                          const Row<NS, VEC, CPLX>& r) {
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    const int slot = lane + 64 * s;
+    if (slot < g.S) {
+      stv<VEC>(base + slot * VEC, r.a[s]);
+      if constexpr (CPLX) stv<VEC>(base + g.half + slot * VEC, r.b[s]);
+    }
+  }
+}
+// RotatE relation rows: K phases, same slot cut as the complex half.
+template <int NS, int VEC>
+__device__ __forceinline__ void load_phase(const float* __restrict__ base, int S, int lane,
+                                           float (&p)[NS][VEC]) {
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    const int slot = lane + 64 * s;
+    if (slot < S) ldv<VEC>(base + slot * VEC, p[s]);
+    else zv<VEC>(p[s]);
+  }
+}
+
+template <int NS, int VEC, bool CPLX>
+__device__ __forceinline__ void zero_row(Row<NS, VEC, CPLX>& r) {
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    zv<VEC>(r.a[s]);
+    if constexpr (CPLX) zv<VEC>(r.b[s]);
+  }
+}
+
+// ------------------------------------------------------------ reductions
+__device__ __forceinline__ float wave_sum(float x) {
+  // xor butterfly: every lane ends with the bit-identical total (IEEE add is
+  // commutative and each level pairs the same two partial sums on both sides).
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
+  return x;
+}
+__device__ __forceinline__ float wave_max(float x) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) x = fmaxf(x, __shfl_xor(x, o, 64));
+  return x;
+}
+
+__device__ __forceinline__ float sgnf(float x) { return (x > 0.f) ? 1.f : ((x < 0.f) ? -1.f : 0.f); }
+
+// F.logsigmoid (ATen CPU: min(x,0) - log1p(exp(-|x|))) and sigmoid.
+__device__ __forceinline__ float log_sigmoid(float x) {
+  return fminf(x, 0.f) - log1pf(expf(-fabsf(x)));
+}
+__device__ __forceinline__ float sigmoidf(float x) { return 1.f / (1.f + expf(-x)); }
+
+// ------------------------------------------------------------ model math
+// q construction for the element (a, b) of one slot.
+//   TAIL/SINGLE: inputs (x = head, r); HEAD: inputs (r, x = tail)
+// For RotatE `ra` is the relation phase-angle element; `rb` is unused.
+template <int M, int MODE>
+struct Elem {
+  static constexpr bool HEAD = (MODE == HEAD_BATCH);
+
+  __device__ static __forceinline__ void make_q(float xa, float xb, float ra, float rb, const Consts& c,
+                                                float& qa, float& qb) {
+    if constexpr (M == TRANSE) {
+      if constexpr (HEAD) qa = ra - xa;   // (relation - tail), model.py:168
+      else qa = xa + ra;                  // (head + relation), model.py:170
+      qb = 0.f;
+    } else if constexpr (M == DISTMULT) {
+      qa = HEAD ? (ra * xa) : (xa * ra);  // model.py:177 / :179
+      qb = 0.f;
+    } else if constexpr (M == COMPLEX) {
+      if constexpr (HEAD) {               // model.py:190-191
+        qa = ra * xa + rb * xb;
+        qb = ra * xb - rb * xa;
+      } else {                            // model.py:194-195
+        qa = xa * ra - xb * rb;
+        qb = xa * rb + xb * ra;
+      }
+    } else if constexpr (M == ROTATE) {
+      const float th = ra / c.kappa;      // true fp32 division, model.py:209
+      float sn, cs;
+      sincosf(th, &sn, &cs);              // model.py:211-212
+      if constexpr (HEAD) {               // model.py:215-216
+        qa = cs * xa + sn * xb;
+        qb = cs * xb - sn * xa;
+      } else {                            // model.py:220-221
+        qa = xa * cs - xb * sn;
+        qb = xa * sn + xb * cs;
+      }
+    } else {                              // PROTATE, model.py:236-243
+      const float pr = ra / c.kappa_p;
+      const float px = xa / c.kappa_p;
+      qa = HEAD ? (pr - px) : (px + pr);
+      qb = 0.f;
+    }
+  }
+
+  // per-element term of the reduction over dim 2
+  __device__ static __forceinline__ float phi(float qa, float qb, float ea, float eb, const Consts& c) {
+    if constexpr (M == TRANSE) {
+      return fabsf(HEAD ? (ea + qa) : (qa - ea));           // torch.norm(p=1), model.py:172
+    } else if constexpr (M == DISTMULT) {
+      return HEAD ? (ea * qa) : (qa * ea);                  // model.py:181
+    } else if constexpr (M == COMPLEX) {
+      return HEAD ? (ea * qa + eb * qb) : (qa * ea + qb * eb);  // model.py:192,196
+    } else if constexpr (M == ROTATE) {
+      const float dr = qa - ea, di = qb - eb;               // model.py:217-223
+      return sqrtf(dr * dr + di * di);                      // stack+norm(dim=0), model.py:225-226
+    } else {
+      const float pe = ea / c.kappa_p;
+      const float x = HEAD ? (pe + qa) : (qa - pe);
+      return fabsf(sinf(x));                                // model.py:245-246
+    }
+  }
+
+  // score from the summed terms
+  __device__ static __forceinline__ float finish(float total, const Consts& c) {
+    if constexpr (M == TRANSE || M == ROTATE) return c.gamma - total;       // model.py:172,228
+    else if constexpr (M == PROTATE) return c.gamma - total * c.modulus;    // model.py:248
+    else return total;                                                       // model.py:181,198
+  }
+
+  // d score / d q and d score / d e for one element
+  __device__ static __forceinline__ void grads(float qa, float qb, float ea, float eb, const Consts& c,
+                                               float& gqa, float& gqb, float& gea, float& geb) {
+    if constexpr (M == TRANSE) {
+      const float v = HEAD ? (ea + qa) : (qa - ea);
+      const float sg = sgnf(v);
+      gqa = -sg;
+      gea = HEAD ? -sg : sg;
+      gqb = geb = 0.f;
+    } else if constexpr (M == DISTMULT) {
+      gqa = ea; gea = qa; gqb = geb = 0.f;
+    } else if constexpr (M == COMPLEX) {
+      gqa = ea; gqb = eb; gea = qa; geb = qb;
+    } else if constexpr (M == ROTATE) {
+      const float dr = qa - ea, di = qb - eb;
+      const float rho = sqrtf(dr * dr + di * di);
+      if (rho > 0.f) {                 // norm backward is masked at 0
+        const float ur = dr / rho, ui = di / rho;
+        gqa = -ur; gqb = -ui; gea = ur; geb = ui;
+      } else {
+        gqa = gqb = gea = geb = 0.f;
+      }
+    } else {
+      const float pe = ea / c.kappa_p;
+      const float x = HEAD ? (pe + qa) : (qa - pe);
+      float sn, cs;
+      sincosf(x, &sn, &cs);
+      const float dx = -c.modulus * sgnf(sn) * cs;
+      gqa = dx;
+      gea = (HEAD ? dx : -dx) / c.kappa_p;
+      gqb = geb = 0.f;
+    }
+  }
+
+  // d score / d modulus = -phi summed (pRotatE only); uses the raw total.
+
+  // chain d q → d x (head for tail/single, tail for head-batch) and d r
+  __device__ static __forceinline__ void chain(float xa, float xb, float ra, float rb, float dqa, float dqb,
+                                               const Consts& c, float& dxa, float& dxb, float& dra,
+                                               float& drb) {
+    if constexpr (M == TRANSE) {
+      dra = dqa;
+      dxa = HEAD ? -dqa : dqa;
+      dxb = drb = 0.f;
+    } else if constexpr (M == DISTMULT) {
+      // tail q = x*r ; head q = r*x
+      dxa = dqa * ra;
+      dra = dqa * xa;
+      dxb = drb = 0.f;
+    } else if constexpr (M == COMPLEX) {
+      if constexpr (HEAD) {
+        // qa = ra xa + rb xb ; qb = ra xb - rb xa   (x = tail)
+        dxa = dqa * ra - dqb * rb;
+        dxb = dqa * rb + dqb * ra;
+        dra = dqa * xa + dqb * xb;
+        drb = dqa * xb - dqb * xa;
+      } else {
+        // qa = xa ra - xb rb ; qb = xa rb + xb ra   (x = head)
+        dxa = dqa * ra + dqb * rb;
+        dxb = dqb * ra - dqa * rb;
+        dra = dqa * xa + dqb * xb;
+        drb = dqb * xa - dqa * xb;
+      }
+    } else if constexpr (M == ROTATE) {
+      const float th = ra / c.kappa;
+      float sn, cs;
+      sincosf(th, &sn, &cs);
+      float dth;
+      if constexpr (HEAD) {
+        // qa = cs xa + sn xb ; qb = cs xb - sn xa
+        dxa = dqa * cs - dqb * sn;
+        dxb = dqa * sn + dqb * cs;
+        const float qa = cs * xa + sn * xb, qb = cs * xb - sn * xa;
+        dth = dqa * qb - dqb * qa;
+      } else {
+        // qa = xa cs - xb sn ; qb = xa sn + xb cs
+        dxa = dqa * cs + dqb * sn;
+        dxb = dqb * cs - dqa * sn;
+        const float qa = xa * cs - xb * sn, qb = xa * sn + xb * cs;
+        dth = dqb * qa - dqa * qb;
+      }
+      dra = dth / c.kappa;
+      drb = 0.f;
+    } else {
+      dra = dqa / c.kappa_p;
+      dxa = HEAD ? -(dqa / c.kappa_p) : (dqa / c.kappa_p);
+      dxb = drb = 0.f;
+    }
+  }
+};
+
+// Sum of phi over the lane's slots (fixed ascending order).
+template <int M, int MODE, int NS, int VEC, bool CPLX>
+__device__ __forceinline__ float lane_total(const Row<NS, VEC, CPLX>& q, const Row<NS, VEC, CPLX>& e,
+                                            const Consts& c) {
+  using EL = Elem<M, MODE>;
+  float acc = 0.f;
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+#pragma unroll
+    for (int v = 0; v < VEC; ++v) {
+      float t;
+      if constexpr (CPLX) t = EL::phi(q.a[s][v], q.b[s][v], e.a[s][v], e.b[s][v], c);
+      else t = EL::phi(q.a[s][v], 0.f, e.a[s][v], 0.f, c);
+      acc += t;
+    }
+  }
+  return acc;
+}
+
+// q for a row: x = head row (tail/single) or tail row (head-batch).
+template <int M, int MODE, int NS, int VEC, bool CPLX>
+__device__ __forceinline__ void build_q(const Row<NS, VEC, CPLX>& x, const Row<NS, VEC, CPLX>& r,
+                                        const Consts& c, Row<NS, VEC, CPLX>& q) {
+  using EL = Elem<M, MODE>;
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+#pragma unroll
+    for (int v = 0; v < VEC; ++v) {
+      float qa, qb;
+      if constexpr (CPLX) EL::make_q(x.a[s][v], x.b[s][v], r.a[s][v], r.b[s][v], c, qa, qb);
+      else EL::make_q(x.a[s][v], 0.f, r.a[s][v], 0.f, c, qa, qb);
+      q.a[s][v] = qa;
+      if constexpr (CPLX) q.b[s][v] = qb;
+    }
+  }
+}
+
+// Load the relation row into a Row: RotatE phases go to `a` (b unused).
+template <int M, int NS, int VEC, bool CPLX>
+__device__ __forceinline__ void load_rel(const float* __restrict__ base, RowGeom eg, int lane,
+                                         Row<NS, VEC, CPLX>& r) {
+  if constexpr (Traits<M>::rel_phase) {
+    load_phase<NS, VEC>(base, eg.S, lane, r.a);
+#pragma unroll
+    for (int s = 0; s < NS; ++s) zv<VEC>(r.b[s]);
+  } else {
+    load_row<NS, VEC, CPLX>(base, eg, lane, r);
+  }
+}
+template <int M, int NS, int VEC, bool CPLX>
+__device__ __forceinline__ void store_rel(float* __restrict__ base, RowGeom eg, int lane,
+                                          const Row<NS, VEC, CPLX>& r) {
+  if constexpr (Traits<M>::rel_phase) {
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      const int slot = lane + 64 * s;
+      if (slot < eg.S) stv<VEC>(base + slot * VEC, r.a[s]);
+    }
+  } else {
+    store_row<NS, VEC, CPLX>(base, eg, lane, r);
+  }
+}
+
+}  // namespace kge

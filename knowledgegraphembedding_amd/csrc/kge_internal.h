@@ -1,0 +1,113 @@
+// kge_internal.h — argument blocks shared by the host dispatcher and the kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <utility>
+
+#include "../../include/kge_hip.h"
+#include "kge_device.h"
+
+namespace kge {
+
+enum RowOp : int { ROW_TRAIN = 0, ROW_GIVEN = 1 };
+
+struct ScoreArgs {
+  const float* ent;
+  const float* rel;
+  const float* modulus;
+  const int64_t* pos;
+  const int64_t* neg;
+  int64_t neg_stride;  // neg index of (i, j) = neg[i * neg_stride + j]
+  int64_t B, n, E, R;
+  int Le, Lr;
+  RowGeom eg;
+  Consts c;
+  int64_t jpw;  // candidates per wave work-unit
+  float* out;
+  int32_t* err;
+};
+
+struct RowArgs {
+  const float* ent;
+  const float* rel;
+  const float* modulus;
+  const int64_t* pos;
+  const int64_t* neg;
+  int64_t neg_stride;
+  int64_t B, n, E, R;
+  int Le, Lr;
+  RowGeom eg;
+  Consts c;
+  int op;           // RowOp
+  int adversarial;  // args.negative_adversarial_sampling
+  float adv_T;      // args.adversarial_temperature
+  int uni_weight;   // args.uni_weight
+  float uni_inv;    // 1 / global batch (uni_weight)
+  const float* sub_w;
+  const float* w_sum;
+  const float* g_in;  // ROW_GIVEN: dL/dscore [B, n]
+  float* g_out;       // ROW_TRAIN: dL/ds_ij [B, n]
+  float* q_out;       // [B, Le]
+  float* ent_contrib; // [2B, Le]  slot 0 = head row, slot 1 = tail row
+  float* rel_contrib; // [B, Lr]
+  float* row_stats;   // [B, 4]  logσ(s_pos), neg term, d/dmodulus, s_pos
+  int n_lds;          // floats reserved for raw scores in LDS (TRAIN: n)
+  int32_t* err;
+};
+
+struct EntArgs {
+  const float* ent;
+  const float* modulus;
+  int64_t E;
+  int Le;
+  RowGeom eg;
+  Consts c;
+  const int32_t* off;   // CSR offsets (entity buckets first)
+  const int32_t* occ;   // occurrence ids, ascending inside each bucket
+  int64_t Bn;           // ids < Bn: negative (i, j) = (id / n, id % n)
+  int64_t n;
+  const float* g;       // [B, n]
+  const float* q;       // [B, Le]
+  const float* ent_contrib;  // ids >= Bn index [2B, Le]
+  float reg3;           // 3 * regularization (0 = off)
+  float* reg_partial;   // [E] Σ|x|^3 per row (when reg3 != 0)
+  float* grad_ent;
+};
+
+struct RankArgs {
+  const float* ent;
+  const float* rel;
+  const float* modulus;
+  const int64_t* queries;
+  int64_t nq, E, R;
+  int Le, Lr;
+  RowGeom eg;
+  Consts c;
+  const int64_t* filt_off;
+  const int64_t* filt_ids;
+  int64_t cpw;          // candidates per wave work-unit
+  float* q;             // [nq, Le]
+  float* s_true;        // [nq]
+  int64_t* true_id;     // [nq]
+  int32_t* gt;          // [nq]
+  int32_t* eq;          // [nq]
+  int64_t* ranks;
+  int32_t* ties;
+  int32_t* err;
+};
+
+struct ModelOps {
+  int (*score)(int mode, int vec, int ns, const ScoreArgs&, int64_t units, hipStream_t);
+  int (*row)(int mode, int vec, int ns, const RowArgs&, size_t lds, hipStream_t);
+  int (*entity)(int mode, int vec, int ns, const EntArgs&, hipStream_t);
+  int (*rank)(int mode, int vec, int ns, const RankArgs&, hipStream_t);
+};
+
+ModelOps model_ops_transe();
+ModelOps model_ops_distmult();
+ModelOps model_ops_complex();
+ModelOps model_ops_rotate();
+ModelOps model_ops_protate();
+
+}  // namespace kge

@@ -1,0 +1,148 @@
+"""TrainDataset / TestDataset / BidirectionalOneShotIterator — the reference's
+data API (codes/dataloader.py), unchanged in behaviour.
+
+TrainDataset draws its negatives with the same numpy calls in the same order
+(dataloader.py:39-61), so a seeded numpy RNG yields the reference's exact
+batches; it remains host-side CPU work feeding the device.
+TestDataset keeps its item format for API users; KGEModel.test_step itself
+ranks through filters.FilterIndex + the ranking kernel instead.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+from torch.utils.data import Dataset
+
+from .filters import FilterIndex
+
+
+class TrainDataset(Dataset):
+    def __init__(self, triples, nentity, nrelation, negative_sample_size, mode):
+        self.len = len(triples)
+        self.triples = triples
+        self.triple_set = set(triples)
+        self.nentity = nentity
+        self.nrelation = nrelation
+        self.negative_sample_size = negative_sample_size
+        self.mode = mode
+        self.count = self.count_frequency(triples)
+        self.true_head, self.true_tail = self.get_true_head_and_tail(self.triples)
+
+    def __len__(self):
+        return self.len
+
+    def __getitem__(self, idx):
+        positive_sample = self.triples[idx]
+        head, relation, tail = positive_sample
+
+        # word2vec-style subsampling weight, fp32 like dataloader.py:33-34
+        subsampling_weight = self.count[(head, relation)] + self.count[(tail, -relation - 1)]
+        subsampling_weight = torch.sqrt(1 / torch.Tensor([subsampling_weight]))
+
+        if self.mode == 'head-batch':
+            true_ids = self.true_head[(relation, tail)]
+        elif self.mode == 'tail-batch':
+            true_ids = self.true_tail[(head, relation)]
+        else:
+            raise ValueError('Training batch mode %s not supported' % self.mode)
+
+        # rejection sampling: draw 2n uniform ids per round, drop the true ones
+        chunks = []
+        have = 0
+        while have < self.negative_sample_size:
+            draw = np.random.randint(self.nentity, size=self.negative_sample_size * 2)
+            draw = draw[np.isin(draw, true_ids, assume_unique=True, invert=True)]
+            chunks.append(draw)
+            have += draw.size
+        negative_sample = torch.from_numpy(np.concatenate(chunks)[:self.negative_sample_size])
+        return torch.LongTensor(positive_sample), negative_sample, subsampling_weight, self.mode
+
+    @staticmethod
+    def collate_fn(data):
+        positive_sample = torch.stack([d[0] for d in data], dim=0)
+        negative_sample = torch.stack([d[1] for d in data], dim=0)
+        subsample_weight = torch.cat([d[2] for d in data], dim=0)
+        return positive_sample, negative_sample, subsample_weight, data[0][3]
+
+    @staticmethod
+    def count_frequency(triples, start=4):
+        '''Frequency of (head, relation) and (tail, -relation-1), starting at `start`.'''
+        count = {}
+        for head, relation, tail in triples:
+            count[(head, relation)] = count.get((head, relation), start - 1) + 1
+            count[(tail, -relation - 1)] = count.get((tail, -relation - 1), start - 1) + 1
+        return count
+
+    @staticmethod
+    def get_true_head_and_tail(triples):
+        '''True heads per (relation, tail) and true tails per (head, relation).'''
+        true_head, true_tail = {}, {}
+        for head, relation, tail in triples:
+            true_tail.setdefault((head, relation), []).append(tail)
+            true_head.setdefault((relation, tail), []).append(head)
+        true_head = {k: np.array(list(set(v))) for k, v in true_head.items()}
+        true_tail = {k: np.array(list(set(v))) for k, v in true_tail.items()}
+        return true_head, true_tail
+
+
+class TestDataset(Dataset):
+    def __init__(self, triples, all_true_triples, nentity, nrelation, mode):
+        self.len = len(triples)
+        self.triple_set = set(all_true_triples)
+        self.triples = triples
+        self.nentity = nentity
+        self.nrelation = nrelation
+        self.mode = mode
+        self._index = FilterIndex(list(self.triple_set), nentity, nrelation) if self.triple_set else None
+
+    def __len__(self):
+        return self.len
+
+    def __getitem__(self, idx):
+        head, relation, tail = self.triples[idx]
+        if self.mode == 'head-batch':
+            true_id = head
+        elif self.mode == 'tail-batch':
+            true_id = tail
+        else:
+            raise ValueError('negative batch mode %s not supported' % self.mode)
+        negative_sample = torch.arange(self.nentity, dtype=torch.int64)
+        filter_bias = torch.zeros(self.nentity, dtype=torch.float32)
+        if self._index is not None:
+            f = torch.from_numpy(self._index.filtered((head, relation, tail), self.mode))
+            negative_sample[f] = true_id  # filtered candidate -> (-1, true id), dataloader.py:138-144
+            filter_bias[f] = -1.0
+        positive_sample = torch.LongTensor((head, relation, tail))
+        return positive_sample, negative_sample, filter_bias, self.mode
+
+    @staticmethod
+    def collate_fn(data):
+        positive_sample = torch.stack([d[0] for d in data], dim=0)
+        negative_sample = torch.stack([d[1] for d in data], dim=0)
+        filter_bias = torch.stack([d[2] for d in data], dim=0)
+        return positive_sample, negative_sample, filter_bias, data[0][3]
+
+
+class BidirectionalOneShotIterator(object):
+    '''Alternates tail-batch (odd steps) and head-batch (even steps) batches.'''
+
+    def __init__(self, dataloader_head, dataloader_tail):
+        self.iterator_head = self.one_shot_iterator(dataloader_head)
+        self.iterator_tail = self.one_shot_iterator(dataloader_tail)
+        self.step = 0
+
+    def __iter__(self):
+        return self
+
+    def __next__(self):
+        self.step += 1
+        if self.step % 2 == 0:
+            return next(self.iterator_head)
+        return next(self.iterator_tail)
+
+    @staticmethod
+    def one_shot_iterator(dataloader):
+        '''Endless iterator over a DataLoader.'''
+        while True:
+            for data in dataloader:
+                yield data

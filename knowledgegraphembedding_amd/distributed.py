@@ -1,0 +1,58 @@
+"""Data-parallel training over one process per GPU (torch.distributed; the
+"nccl" backend is RCCL on ROCm, gloo on CPU for tests).
+
+The reference is single-device.  Sharding the positive
+batch across ranks changes nothing in the maths as long as the loss
+normaliser is global: every rank
+
+  1. all-reduces Σw (one scalar) so c_i = w_i / Σw_global (model.py:285-286),
+     or uses 1 / (B * world) under --uni_weight;
+  2. runs the fused kernel on its shard → dense partial gradients;
+  3. all-reduces (SUM) the entity/relation(/modulus) gradients and the four
+     loss partials in one flat bucket list;
+  4. steps the (replicated) optimizer identically.
+
+The regularisation term reads the full tables, so only rank 0 adds it before
+the sum (it would otherwise be counted world_size times).
+"""
+from __future__ import annotations
+
+import copy
+
+import torch
+import torch.distributed as dist
+
+
+def dp_allreduce_(tensors, group=None) -> None:
+    """In-place SUM all-reduce of a list of tensors (one collective per tensor;
+    RCCL runs them on its own stream in issue order)."""
+    for t in tensors:
+        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+
+
+def dp_weight_sum(subsampling_weight: torch.Tensor, group=None) -> torch.Tensor:
+    ws = subsampling_weight.float().sum().reshape(1)
+    dist.all_reduce(ws, op=dist.ReduceOp.SUM, group=group)
+    return ws
+
+
+def dp_train_grads(model, positive_sample, negative_sample, subsampling_weight, mode, args):
+    """Fused per-rank gradients + global reduction; returns the global [4] loss vector."""
+    group = args.dp_group
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    B = positive_sample.shape[0]
+    wsum = None if args.uni_weight else dp_weight_sum(subsampling_weight, group)
+    local_args = args
+    if rank != 0 and args.regularization != 0.0:
+        local_args = copy.copy(args)
+        local_args.regularization = 0.0
+    losses = model.compute_train_grads(positive_sample, negative_sample, subsampling_weight, mode, local_args,
+                                       weight_sum=wsum, uni_batch=B * world)
+    grads = [model.entity_embedding.grad, model.relation_embedding.grad]
+    if model.model_name == 'pRotatE' and model.modulus.grad is not None:
+        grads.append(model.modulus.grad)
+    dp_allreduce_(grads + [losses], group)
+    # loss = (pos + neg) / 2 + reg must be recomputed from the summed parts
+    losses[2] = (losses[0] + losses[1]) / 2 + losses[3]
+    return losses

@@ -1,0 +1,59 @@
+"""Host-side index of true triples for filtered ranking.
+
+The reference builds, per test query, an nentity-long Python list in which
+every candidate that forms a true triple (all_true_triples = train + valid +
+test, run.py:225) is replaced by (-1, true_id) (dataloader.py:134-154).  Here
+the same set is kept as two sorted arrays (tails by (h, r), heads by (r, t))
+and handed to the ranking kernel as a CSR of the filtered candidate ids of
+each query — the true entity itself excluded, exactly as tmp[head] /
+tmp[tail] = (0, id) re-admits it (dataloader.py:140, 144).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+
+class FilterIndex:
+    def __init__(self, all_true_triples, nentity: int, nrelation: int):
+        t = np.asarray(all_true_triples, dtype=np.int64).reshape(-1, 3)
+        t = np.unique(t, axis=0)  # set(all_true_triples), dataloader.py:125
+        self.nentity = int(nentity)
+        self.nrelation = int(nrelation)
+        R, E = self.nrelation, self.nentity
+        k_hr = t[:, 0] * R + t[:, 1]
+        o = np.lexsort((t[:, 2], k_hr))
+        self._k_hr, self._tails = k_hr[o], t[o, 2]
+        k_rt = t[:, 1] * E + t[:, 2]
+        o = np.lexsort((t[:, 0], k_rt))
+        self._k_rt, self._heads = k_rt[o], t[o, 0]
+
+    def filter_csr(self, queries, mode: str):
+        """(offsets [nq+1] int64, ids int64) of the filtered candidates per query."""
+        q = np.asarray(queries, dtype=np.int64).reshape(-1, 3)
+        if mode == 'tail-batch':
+            keys, vals, cand = q[:, 0] * self.nrelation + q[:, 1], self._tails, self._k_hr
+            true = q[:, 2]
+        elif mode == 'head-batch':
+            keys, vals, cand = q[:, 1] * self.nentity + q[:, 2], self._heads, self._k_rt
+            true = q[:, 0]
+        else:
+            raise ValueError('negative batch mode %s not supported' % mode)
+        lo = np.searchsorted(cand, keys, side='left')
+        hi = np.searchsorted(cand, keys, side='right')
+        cnt = hi - lo
+        total = int(cnt.sum())
+        if total == 0:
+            return np.zeros(len(q) + 1, dtype=np.int64), np.zeros(0, dtype=np.int64)
+        starts = np.repeat(lo - np.concatenate(([0], np.cumsum(cnt)[:-1])), cnt)
+        ids = vals[starts + np.arange(total)]
+        owner = np.repeat(np.arange(len(q)), cnt)
+        keep = ids != true[owner]
+        ids, owner = ids[keep], owner[keep]
+        per = np.bincount(owner, minlength=len(q))
+        off = np.zeros(len(q) + 1, dtype=np.int64)
+        np.cumsum(per, out=off[1:])
+        return off, ids.astype(np.int64)
+
+    def filtered(self, triple, mode: str) -> np.ndarray:
+        off, ids = self.filter_csr([triple], mode)
+        return ids[off[0]:off[1]]

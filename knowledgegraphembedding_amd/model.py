@@ -1,0 +1,330 @@
+"""KGEModel — drop-in for codes/model.py:KGEModel, computing on MI355X.
+
+Public surface kept from the reference:
+  KGEModel(model_name, nentity, nrelation, hidden_dim, gamma,
+           double_entity_embedding=False, double_relation_embedding=False)   model.py:22-70
+  KGEModel.forward(sample, mode='single') -> [B, n] scores                    model.py:72-164
+  KGEModel.TransE/DistMult/ComplEx/RotatE/pRotatE(head, relation, tail, mode)  model.py:166-249
+  KGEModel.train_step(model, optimizer, train_iterator, args) -> log dict      model.py:252-312
+  KGEModel.test_step(model, test_triples, all_true_triples, args) -> metrics   model.py:315-429
+
+Parameters, their names, shapes, init and state_dict keys are the
+reference's (gamma, embedding_range, entity_embedding, relation_embedding,
+modulus), so reference checkpoints load unchanged.  All scoring, loss,
+gradient and ranking arithmetic runs in libkge_hip.so (see ops.py); CPU
+tensors are rejected instead of silently falling back.
+"""
+from __future__ import annotations
+
+import logging
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+from . import ops
+from .filters import FilterIndex
+
+_MODELS = ['TransE', 'DistMult', 'ComplEx', 'RotatE', 'pRotatE']
+
+
+class _TableScore(torch.autograd.Function):
+    """score = kge_score(tables, indices); backward = kge_score_backward (dense grads)."""
+
+    @staticmethod
+    def forward(ctx, entity, relation, modulus, pos, neg, mode, name, gamma, erange):
+        dev = ops._require_device(entity, relation, pos, neg if neg is not None else pos)
+        desc = ops.make_desc(name, entity.detach(), relation.detach(), gamma, erange,
+                             None if modulus is None else modulus.detach())
+        out = ops.score(desc, mode, pos, neg, dev)
+        ctx.save_for_backward(entity, relation, modulus if modulus is not None else entity.new_empty(0), pos,
+                              neg if neg is not None else pos.new_empty(0))
+        ctx.meta = (mode, name, gamma, erange, modulus is not None)
+        return out
+
+    @staticmethod
+    def backward(ctx, grad_out):
+        entity, relation, modulus, pos, neg = ctx.saved_tensors
+        mode, name, gamma, erange, has_mod = ctx.meta
+        dev = entity.device
+        desc = ops.make_desc(name, entity.detach(), relation.detach(), gamma, erange, modulus if has_mod else None)
+        ge, gr, gm = ops.score_backward(desc, mode, pos, None if mode == 'single' else neg, grad_out, dev, has_mod)
+        return ge, gr, (gm.view_as(modulus) if has_mod else None), None, None, None, None, None, None
+
+
+class KGEModel(nn.Module):
+    def __init__(self, model_name, nentity, nrelation, hidden_dim, gamma,
+                 double_entity_embedding=False, double_relation_embedding=False):
+        super(KGEModel, self).__init__()
+        self.model_name = model_name
+        self.nentity = nentity
+        self.nrelation = nrelation
+        self.hidden_dim = hidden_dim
+        self.epsilon = 2.0
+
+        # model.py:32-40 — fp32 scalars; .item() of them is what the reference's math reads
+        self.gamma = nn.Parameter(torch.Tensor([gamma]), requires_grad=False)
+        self.embedding_range = nn.Parameter(
+            torch.Tensor([(self.gamma.item() + self.epsilon) / hidden_dim]), requires_grad=False)
+
+        self.entity_dim = hidden_dim * 2 if double_entity_embedding else hidden_dim
+        self.relation_dim = hidden_dim * 2 if double_relation_embedding else hidden_dim
+
+        # model.py:45-57 — same draws from torch's CPU generator as the reference
+        r = self.embedding_range.item()
+        self.entity_embedding = nn.Parameter(torch.zeros(nentity, self.entity_dim))
+        nn.init.uniform_(tensor=self.entity_embedding, a=-r, b=r)
+        self.relation_embedding = nn.Parameter(torch.zeros(nrelation, self.relation_dim))
+        nn.init.uniform_(tensor=self.relation_embedding, a=-r, b=r)
+
+        if model_name == 'pRotatE':
+            self.modulus = nn.Parameter(torch.Tensor([[0.5 * r]]))
+
+        if model_name not in _MODELS:
+            raise ValueError('model %s not supported' % model_name)
+        if model_name == 'RotatE' and (not double_entity_embedding or double_relation_embedding):
+            raise ValueError('RotatE should use --double_entity_embedding')
+        if model_name == 'ComplEx' and (not double_entity_embedding or not double_relation_embedding):
+            raise ValueError('ComplEx should use --double_entity_embedding and --double_relation_embedding')
+
+        self._scalars = None
+        self._grad_bufs = None
+
+    # ------------------------------------------------------------------ helpers
+    def _host_scalars(self):
+        """(gamma, embedding_range) as Python floats, cached (they never train)."""
+        if self._scalars is None:
+            self._scalars = (float(self.gamma.detach().cpu().item()),
+                             float(self.embedding_range.detach().cpu().item()))
+        return self._scalars
+
+    def _load_from_state_dict(self, *args, **kwargs):
+        self._scalars = None
+        return super()._load_from_state_dict(*args, **kwargs)
+
+    def _modulus(self):
+        return self.modulus if self.model_name == 'pRotatE' else None
+
+    def desc(self):
+        g, rng = self._host_scalars()
+        mod = self._modulus()
+        return ops.make_desc(self.model_name, self.entity_embedding.detach(), self.relation_embedding.detach(), g, rng,
+                             None if mod is None else mod.detach())
+
+    # ------------------------------------------------------------------ forward
+    def forward(self, sample, mode='single'):
+        '''Scores of a batch (model.py:72-164).
+
+        'single': sample = triples [B, 3] -> [B, 1]
+        'head-batch': sample = (tail_part [B, 3], head_part [B, n]) -> [B, n]
+        'tail-batch': sample = (head_part [B, 3], tail_part [B, n]) -> [B, n]
+        '''
+        if mode == 'single':
+            pos, neg = sample, None
+        elif mode == 'head-batch':
+            pos, neg = sample
+        elif mode == 'tail-batch':
+            pos, neg = sample
+        else:
+            raise ValueError('mode %s not supported' % mode)
+        dev = self.entity_embedding.device
+        pos = pos.to(dev)
+        neg = None if neg is None else neg.to(dev)
+        g, rng = self._host_scalars()
+        score = _TableScore.apply(self.entity_embedding, self.relation_embedding, self._modulus(), pos, neg, mode,
+                                  self.model_name, g, rng)
+        return score
+
+    # ------------------------------------------------------- score plug-ins
+    def _plugin(self, name, head, relation, tail, mode):
+        """Plug-in call on gathered rows (model.py:151-160): the rows become
+        small tables and go through the same HIP score kernel (with autograd)."""
+        B = relation.shape[0]
+        if mode == 'head-batch':
+            n = head.shape[1]
+            ent = torch.cat([head.reshape(B * n, -1), tail.reshape(B, -1)], 0)
+            neg = torch.arange(B * n, device=ent.device).view(B, n)
+            tid = torch.arange(B, device=ent.device) + B * n
+            pos = torch.stack([tid, torch.arange(B, device=ent.device), tid], 1)
+        elif mode == 'tail-batch':
+            n = tail.shape[1]
+            ent = torch.cat([tail.reshape(B * n, -1), head.reshape(B, -1)], 0)
+            neg = torch.arange(B * n, device=ent.device).view(B, n)
+            hid = torch.arange(B, device=ent.device) + B * n
+            pos = torch.stack([hid, torch.arange(B, device=ent.device), hid], 1)
+        elif mode == 'single':
+            ent = torch.cat([head.reshape(B, -1), tail.reshape(B, -1)], 0)
+            neg = None
+            ar = torch.arange(B, device=ent.device)
+            pos = torch.stack([ar, ar, ar + B], 1)
+        else:
+            raise ValueError('mode %s not supported' % mode)
+        g, rng = self._host_scalars()
+        return _TableScore.apply(ent.contiguous(), relation.reshape(B, -1).contiguous(), self._modulus(), pos, neg,
+                                 mode, name, g, rng)
+
+    def TransE(self, head, relation, tail, mode):
+        return self._plugin('TransE', head, relation, tail, mode)
+
+    def DistMult(self, head, relation, tail, mode):
+        return self._plugin('DistMult', head, relation, tail, mode)
+
+    def ComplEx(self, head, relation, tail, mode):
+        return self._plugin('ComplEx', head, relation, tail, mode)
+
+    def RotatE(self, head, relation, tail, mode):
+        return self._plugin('RotatE', head, relation, tail, mode)
+
+    def pRotatE(self, head, relation, tail, mode):
+        return self._plugin('pRotatE', head, relation, tail, mode)
+
+    # --------------------------------------------------------------- training
+    def _grad_buffers(self):
+        dev = self.entity_embedding.device
+        bufs = self._grad_bufs
+        if bufs is None or bufs[0].device != dev or bufs[0].shape != self.entity_embedding.shape:
+            ge = torch.empty_like(self.entity_embedding, memory_format=torch.contiguous_format)
+            gr = torch.empty_like(self.relation_embedding, memory_format=torch.contiguous_format)
+            gm = torch.empty(1, 1, device=dev) if self.model_name == 'pRotatE' else None
+            losses = torch.empty(4, device=dev)
+            self._grad_bufs = bufs = (ge, gr, gm, losses)
+        return bufs
+
+    def compute_train_grads(self, positive_sample, negative_sample, subsampling_weight, mode, args,
+                            weight_sum=None, uni_batch=0):
+        """Fused forward + self-adversarial loss + backward (model.py:268-301).
+        Writes dense .grad tensors; returns the device [4] loss vector
+        (positive_sample_loss, negative_sample_loss, loss, regularization)."""
+        dev = ops._require_device(self.entity_embedding)
+        g, rng = self._host_scalars()
+        ge, gr, gm, losses = self._grad_buffers()
+        ops.train_step_grads(
+            self.desc(), mode, positive_sample, negative_sample, subsampling_weight, dev,
+            adversarial=bool(args.negative_adversarial_sampling),
+            temperature=float(getattr(args, 'adversarial_temperature', 1.0)),
+            uni_weight=bool(args.uni_weight), regularization=float(args.regularization),
+            grad_entity=ge, grad_relation=gr, grad_modulus=gm, losses=losses,
+            weight_sum_dev=weight_sum, uni_batch=uni_batch)
+        if self.entity_embedding.requires_grad:
+            self.entity_embedding.grad = ge
+        if self.relation_embedding.requires_grad:
+            self.relation_embedding.grad = gr
+        if gm is not None and self.modulus.requires_grad:
+            self.modulus.grad = gm
+        return losses
+
+    @staticmethod
+    def train_step(model, optimizer, train_iterator, args):
+        '''
+        A single train step. Apply back-propation and return the loss
+        (model.py:252-312).  One fused HIP pass replaces the two forward
+        calls, the loss and loss.backward(); one 4-float D2H copy replaces
+        the three .item() syncs.
+        '''
+        model.train()
+        optimizer.zero_grad()
+        positive_sample, negative_sample, subsampling_weight, mode = next(train_iterator)
+        dev = model.entity_embedding.device
+        positive_sample = positive_sample.to(dev, non_blocking=True)
+        negative_sample = negative_sample.to(dev, non_blocking=True)
+        subsampling_weight = subsampling_weight.to(dev, non_blocking=True)
+
+        dp = getattr(args, 'dp_group', None)
+        if dp is not None:
+            from .distributed import dp_train_grads
+            losses = dp_train_grads(model, positive_sample, negative_sample, subsampling_weight, mode, args)
+        else:
+            losses = model.compute_train_grads(positive_sample, negative_sample, subsampling_weight, mode, args)
+
+        optimizer.step()
+
+        vals = losses.cpu().tolist()
+        ops.raise_on_device_error(dev)
+        log = {}
+        if args.regularization != 0.0:
+            log['regularization'] = vals[3]
+        log['positive_sample_loss'] = vals[0]
+        log['negative_sample_loss'] = vals[1]
+        log['loss'] = vals[2]
+        return log
+
+    # ------------------------------------------------------------- evaluation
+    @staticmethod
+    def test_step(model, test_triples, all_true_triples, args):
+        '''
+        Evaluate the model on test or valid datasets (model.py:315-429).
+        '''
+        model.eval()
+        dev = ops._require_device(model.entity_embedding)
+
+        if args.countries:
+            from sklearn.metrics import average_precision_score
+            # AUC-PR over every (test triple, region) pair, model.py:322-344
+            sample = []
+            y_true = []
+            for head, relation, tail in test_triples:
+                for candidate_region in args.regions:
+                    y_true.append(1 if candidate_region == tail else 0)
+                    sample.append((head, relation, candidate_region))
+            sample = torch.LongTensor(sample).to(dev)
+            with torch.no_grad():
+                y_score = model(sample).squeeze(1).cpu().numpy()
+            y_true = np.array(y_true)
+            auc_pr = average_precision_score(y_true, y_score)
+            return {'auc_pr': auc_pr}
+
+        # Filtered MRR / MR / HITS@{1,3,10}: head-batch queries, then tail-batch
+        # (model.py:349-418); the filter is dataloader.py:134-154's.
+        index = FilterIndex(all_true_triples, args.nentity, args.nrelation)
+        triples = np.asarray(test_triples, dtype=np.int64).reshape(-1, 3)
+        desc = model.desc()
+        logs = []
+        test_batch_size = max(1, int(args.test_batch_size))
+        total_steps = 2 * ((len(triples) + test_batch_size - 1) // test_batch_size)
+        test_log_steps = max(1, int(getattr(args, 'test_log_steps', 1000)))
+        block = max(test_batch_size, 256)  # queries per kernel launch; results do not depend on it
+        step = 0
+        with torch.no_grad():
+            for mode in ('head-batch', 'tail-batch'):
+                ranks_all = []
+                for b0 in range(0, len(triples), block):
+                    q = triples[b0:b0 + block]
+                    off, ids = index.filter_csr(q, mode)
+                    ranks, _ = ops.rank_filtered(desc, mode, torch.from_numpy(q), torch.from_numpy(off),
+                                                 torch.from_numpy(ids), dev)
+                    ranks_all.append(ranks)
+                    # progress messages on the reference's batch cadence
+                    nb = (len(q) + test_batch_size - 1) // test_batch_size
+                    for _ in range(nb):
+                        if step % test_log_steps == 0:
+                            logging.info('Evaluating the model... (%d/%d)' % (step, total_steps))
+                        step += 1
+                ranks_np = torch.cat(ranks_all).cpu().numpy() if ranks_all else np.zeros(0, np.int64)
+                ops.raise_on_device_error(dev)
+                for ranking in ranks_np.tolist():
+                    logs.append({
+                        'MRR': 1.0 / ranking,
+                        'MR': float(ranking),
+                        'HITS@1': 1.0 if ranking <= 1 else 0.0,
+                        'HITS@3': 1.0 if ranking <= 3 else 0.0,
+                        'HITS@10': 1.0 if ranking <= 10 else 0.0,
+                    })
+        metrics = {}
+        for metric in logs[0].keys():
+            metrics[metric] = sum([log[metric] for log in logs]) / len(logs)
+        return metrics
+
+    def rank_queries(self, triples, all_true_triples, mode):
+        """Per-query filtered ranks and tie counts (numpy int64, int32) — the
+        quantity test_step averages; exposed for parity tests and tools."""
+        dev = ops._require_device(self.entity_embedding)
+        index = all_true_triples if isinstance(all_true_triples, FilterIndex) else \
+            FilterIndex(all_true_triples, self.nentity, self.nrelation)
+        q = np.asarray(triples, dtype=np.int64).reshape(-1, 3)
+        off, ids = index.filter_csr(q, mode)
+        with torch.no_grad():
+            ranks, ties = ops.rank_filtered(self.desc(), mode, torch.from_numpy(q), torch.from_numpy(off),
+                                            torch.from_numpy(ids), dev)
+        r, t = ranks.cpu().numpy(), ties.cpu().numpy()
+        ops.raise_on_device_error(dev)
+        return r, t

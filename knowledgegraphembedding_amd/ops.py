@@ -1,0 +1,236 @@
+"""Torch-facing wrappers of the HIP entry points (include/kge_hip.h).
+
+PyTorch supplies device memory and the current HIP stream; every FLOP of the
+hot path runs in libkge_hip.so.  Tensors must live on a ROCm device: there is
+deliberately no CPU path (a CPU fallback would void the parity claims).
+"""
+from __future__ import annotations
+
+import math
+from typing import Optional
+
+import torch
+
+from . import _lib
+
+PI = 3.14159265358979323846   # model.py:202
+PI_TYPO = 3.14159262358979323846  # model.py:232 (pRotatE; reproduced on purpose)
+
+
+def _require_device(*ts: torch.Tensor) -> torch.device:
+    dev = None
+    for t in ts:
+        if t is None:
+            continue
+        if t.device.type != "cuda":
+            raise RuntimeError(
+                "knowledgegraphembedding_amd runs on MI355X (ROCm) only: got a tensor on "
+                f"{t.device}. Move the model and batch to the GPU (run.py --cuda)."
+            )
+        if dev is None:
+            dev = t.device
+        elif t.device != dev:
+            raise RuntimeError(f"tensors on different devices: {dev} vs {t.device}")
+    return dev
+
+
+def _ptr(t: Optional[torch.Tensor]):
+    return None if t is None else t.data_ptr()
+
+
+def _stream(dev: torch.device) -> int:
+    return torch.cuda.current_stream(dev).cuda_stream
+
+
+class _DeviceState:
+    """Per-device scratch: a growable workspace and the device error flag."""
+
+    def __init__(self, dev: torch.device):
+        self.dev = dev
+        self.ws = torch.empty(0, dtype=torch.uint8, device=dev)
+        self.err = torch.zeros(1, dtype=torch.int32, device=dev)
+
+    def workspace(self, nbytes: int) -> torch.Tensor:
+        if self.ws.numel() < nbytes:
+            self.ws = torch.empty(int(nbytes * 1.25) + 4096, dtype=torch.uint8, device=self.dev)
+        return self.ws
+
+
+_STATES: dict = {}
+
+
+def state(dev: torch.device) -> _DeviceState:
+    key = (dev.type, dev.index if dev.index is not None else torch.cuda.current_device())
+    st = _STATES.get(key)
+    if st is None:
+        st = _STATES[key] = _DeviceState(torch.device("cuda", key[1]))
+    return st
+
+
+def raise_on_device_error(dev: torch.device) -> None:
+    """Read (and clear) the device error flag — a sync point."""
+    st = state(dev)
+    v = int(st.err.item())
+    if v:
+        st.err.zero_()
+        if v & _lib.DEVERR_INDEX:
+            raise IndexError("index out of range in self")  # what index_select raises (model.py:86-146)
+        raise RuntimeError(f"device error flag {v}")
+
+
+def phase_divisors(embedding_range: float) -> tuple[float, float]:
+    """(range/pi, range/pi') in double, as model.py:209 / :236 compute them."""
+    return embedding_range / PI, embedding_range / PI_TYPO
+
+
+def make_desc(model_name: str, entity: torch.Tensor, relation: torch.Tensor, gamma: float, embedding_range: float,
+              modulus: Optional[torch.Tensor]) -> _lib.ModelDesc:
+    if model_name not in _lib.MODEL_IDS:
+        raise ValueError("model %s not supported" % model_name)
+    if entity.dtype != torch.float32 or relation.dtype != torch.float32:
+        raise TypeError("embeddings must be float32 (model.py:45,52)")
+    if not (entity.is_contiguous() and relation.is_contiguous()):
+        raise ValueError("embeddings must be contiguous")
+    k, kp = phase_divisors(embedding_range)
+    d = _lib.ModelDesc()
+    d.model = _lib.MODEL_IDS[model_name]
+    d.entity_dim = entity.shape[1]
+    d.relation_dim = relation.shape[1]
+    d.nentity = entity.shape[0]
+    d.nrelation = relation.shape[0]
+    d.gamma = gamma
+    d.phase_divisor = k
+    d.phase_divisor_p = kp
+    d.entity_embedding = entity.data_ptr()
+    d.relation_embedding = relation.data_ptr()
+    d.modulus = modulus.data_ptr() if modulus is not None else None
+    return d
+
+
+def _idx(t: torch.Tensor, dev) -> torch.Tensor:
+    if t.device != dev:
+        t = t.to(dev, non_blocking=True)
+    if t.dtype != torch.int64:
+        t = t.long()
+    return t.contiguous()
+
+
+def score(desc: _lib.ModelDesc, mode: str, pos: torch.Tensor, neg: Optional[torch.Tensor], dev) -> torch.Tensor:
+    """Scores [B, n] (model.py:72-249)."""
+    if mode not in _lib.MODE_IDS:
+        raise ValueError("mode %s not supported" % mode)
+    pos = _idx(pos, dev)
+    if mode == "single":
+        B, n = pos.shape[0], 1
+        neg = None
+    else:
+        neg = _idx(neg, dev)
+        B, n = neg.shape[0], neg.shape[1]
+    out = torch.empty(B, n, dtype=torch.float32, device=dev)
+    st = state(dev)
+    lib = _lib.load()
+    _lib.check(
+        lib.kge_score(desc, _lib.MODE_IDS[mode], pos.data_ptr(), _ptr(neg), B, n, out.data_ptr(),
+                      st.err.data_ptr(), _stream(dev)),
+        "kge_score",
+    )
+    return out
+
+
+def score_backward(desc: _lib.ModelDesc, mode: str, pos: torch.Tensor, neg: Optional[torch.Tensor],
+                   grad_scores: torch.Tensor, dev, with_modulus: bool):
+    pos = _idx(pos, dev)
+    if mode == "single":
+        neg = None
+        B, n = pos.shape[0], 1
+    else:
+        neg = _idx(neg, dev)
+        B, n = neg.shape
+    g = grad_scores.to(torch.float32).contiguous().view(B, n)
+    ge = torch.empty(desc.nentity, desc.entity_dim, dtype=torch.float32, device=dev)
+    gr = torch.empty(desc.nrelation, desc.relation_dim, dtype=torch.float32, device=dev)
+    gm = torch.empty(1, 1, dtype=torch.float32, device=dev) if with_modulus else None
+    lib = _lib.load()
+    m = _lib.MODE_IDS[mode]
+    need = lib.kge_backward_workspace_bytes(desc, m, B, n)
+    st = state(dev)
+    ws = st.workspace(need)
+    _lib.check(
+        lib.kge_score_backward(desc, m, pos.data_ptr(), _ptr(neg), B, n, g.data_ptr(), ge.data_ptr(), gr.data_ptr(),
+                               _ptr(gm), ws.data_ptr(), ws.numel(), st.err.data_ptr(), _stream(dev)),
+        "kge_score_backward",
+    )
+    return ge, gr, gm
+
+
+def weight_sum(w: torch.Tensor, out: torch.Tensor) -> None:
+    dev = w.device
+    _lib.check(_lib.load().kge_weight_sum(w.data_ptr(), w.numel(), out.data_ptr(), _stream(dev)), "kge_weight_sum")
+
+
+def train_step_grads(desc: _lib.ModelDesc, mode: str, pos: torch.Tensor, neg: torch.Tensor, sub_w: torch.Tensor,
+                     dev, *, adversarial: bool, temperature: float, uni_weight: bool, regularization: float,
+                     grad_entity: torch.Tensor, grad_relation: torch.Tensor, grad_modulus: Optional[torch.Tensor],
+                     losses: torch.Tensor, weight_sum_dev: Optional[torch.Tensor] = None,
+                     uni_batch: int = 0) -> None:
+    """Fused scoring + loss + backward into the given dense grad buffers (model.py:252-301)."""
+    if mode not in ("head-batch", "tail-batch"):
+        raise ValueError("Training batch mode %s not supported" % mode)
+    pos = _idx(pos, dev)
+    neg = _idx(neg, dev)
+    w = sub_w.to(dev, dtype=torch.float32, non_blocking=True).contiguous().view(-1)
+    B, n = neg.shape
+    lib = _lib.load()
+    need = lib.kge_train_workspace_bytes(desc, B, n)
+    st = state(dev)
+    ws = st.workspace(need)
+    _lib.check(
+        lib.kge_train_step_grads(
+            desc, _lib.MODE_IDS[mode], pos.data_ptr(), neg.data_ptr(), B, n, w.data_ptr(), _ptr(weight_sum_dev),
+            int(bool(uni_weight)), int(uni_batch), int(bool(adversarial)), float(temperature), float(regularization),
+            grad_entity.data_ptr(), grad_relation.data_ptr(), _ptr(grad_modulus), losses.data_ptr(), ws.data_ptr(),
+            ws.numel(), st.err.data_ptr(), _stream(dev)),
+        "kge_train_step_grads",
+    )
+
+
+def adam_step(param: torch.Tensor, grad: torch.Tensor, exp_avg: torch.Tensor, exp_avg_sq: torch.Tensor, *,
+              step: int, lr: float, beta1: float, beta2: float, eps: float) -> None:
+    """torch.optim.Adam's update for one tensor (bias corrections in double, like torch)."""
+    bc1 = 1 - beta1 ** step
+    bc2 = 1 - beta2 ** step
+    step_size = lr / bc1
+    bc2_sqrt = math.sqrt(bc2)
+    dev = _require_device(param, grad, exp_avg, exp_avg_sq)
+    for t in (param, grad, exp_avg, exp_avg_sq):
+        if not t.is_contiguous() or t.dtype != torch.float32:
+            raise ValueError("adam tensors must be contiguous float32")
+    _lib.check(
+        _lib.load().kge_adam_step(param.data_ptr(), grad.data_ptr(), exp_avg.data_ptr(), exp_avg_sq.data_ptr(),
+                                  param.numel(), beta1, beta2, eps, step_size, bc2_sqrt, _stream(dev)),
+        "kge_adam_step",
+    )
+
+
+def rank_filtered(desc: _lib.ModelDesc, mode: str, queries: torch.Tensor, filt_off: torch.Tensor,
+                  filt_ids: torch.Tensor, dev):
+    """Filtered ranks (int64) and tie counts for a block of queries (model.py:383-418)."""
+    if mode not in ("head-batch", "tail-batch"):
+        raise ValueError("mode %s not supported" % mode)
+    q = _idx(queries, dev)
+    off = _idx(filt_off, dev)
+    ids = _idx(filt_ids, dev) if filt_ids.numel() else torch.zeros(1, dtype=torch.int64, device=dev)
+    nq = q.shape[0]
+    ranks = torch.empty(nq, dtype=torch.int64, device=dev)
+    ties = torch.empty(nq, dtype=torch.int32, device=dev)
+    lib = _lib.load()
+    need = lib.kge_rank_workspace_bytes(desc, nq)
+    st = state(dev)
+    ws = st.workspace(need)
+    _lib.check(
+        lib.kge_rank_filtered(desc, _lib.MODE_IDS[mode], q.data_ptr(), nq, off.data_ptr(), ids.data_ptr(),
+                              ranks.data_ptr(), ties.data_ptr(), ws.data_ptr(), ws.numel(), st.err.data_ptr(),
+                              _stream(dev)),
+        "kge_rank_filtered",
+    )
+    return ranks, ties

@@ -1,0 +1,306 @@
+#!/usr/bin/python3
+"""Training / evaluation CLI — the reference's codes/run.py, flag for flag.
+
+    python -m knowledgegraphembedding_amd.run --do_train --cuda --do_valid --do_test \
+        --data_path data/FB15k --model RotatE -n 256 -b 1024 -d 1000 -g 24.0 -a 1.0 -adv \
+        -lr 0.0001 --max_steps 150000 -save models/RotatE_FB15k_0 --test_batch_size 16 -de
+
+Differences from the reference, all on the execution side:
+  * compute runs on the GPU through libkge_hip.so (there is no CPU path;
+    --cuda is implied when a GPU is present and required otherwise);
+  * the optimizer is KGEAdam (torch.optim.Adam's update, fused), state-dict
+    compatible with the reference's checkpoints;
+  * under torchrun (WORLD_SIZE > 1) every rank trains on its own -b batch and
+    gradients are all-reduced over RCCL (knowledgegraphembedding_amd.distributed);
+    rank 0 logs, validates and saves.
+"""
+from __future__ import absolute_import, division, print_function
+
+import argparse
+import json
+import logging
+import os
+
+import numpy as np
+import torch
+from torch.utils.data import DataLoader
+
+from .dataloader import BidirectionalOneShotIterator, TrainDataset
+from .model import KGEModel
+from .optim import KGEAdam
+
+
+def parse_args(args=None):
+    parser = argparse.ArgumentParser(
+        description='Training and Testing Knowledge Graph Embedding Models',
+        usage='train.py [<args>] [-h | --help]'
+    )
+    parser.add_argument('--cuda', action='store_true', help='use GPU')
+    parser.add_argument('--do_train', action='store_true')
+    parser.add_argument('--do_valid', action='store_true')
+    parser.add_argument('--do_test', action='store_true')
+    parser.add_argument('--evaluate_train', action='store_true', help='Evaluate on training data')
+    parser.add_argument('--countries', action='store_true', help='Use Countries S1/S2/S3 datasets')
+    parser.add_argument('--regions', type=int, nargs='+', default=None,
+                        help='Region Id for Countries S1/S2/S3 datasets, DO NOT MANUALLY SET')
+    parser.add_argument('--data_path', type=str, default=None)
+    parser.add_argument('--model', default='TransE', type=str)
+    parser.add_argument('-de', '--double_entity_embedding', action='store_true')
+    parser.add_argument('-dr', '--double_relation_embedding', action='store_true')
+    parser.add_argument('-n', '--negative_sample_size', default=128, type=int)
+    parser.add_argument('-d', '--hidden_dim', default=500, type=int)
+    parser.add_argument('-g', '--gamma', default=12.0, type=float)
+    parser.add_argument('-adv', '--negative_adversarial_sampling', action='store_true')
+    parser.add_argument('-a', '--adversarial_temperature', default=1.0, type=float)
+    parser.add_argument('-b', '--batch_size', default=1024, type=int)
+    parser.add_argument('-r', '--regularization', default=0.0, type=float)
+    parser.add_argument('--test_batch_size', default=4, type=int, help='valid/test batch size')
+    parser.add_argument('--uni_weight', action='store_true',
+                        help='Otherwise use subsampling weighting like in word2vec')
+    parser.add_argument('-lr', '--learning_rate', default=0.0001, type=float)
+    parser.add_argument('-cpu', '--cpu_num', default=10, type=int)
+    parser.add_argument('-init', '--init_checkpoint', default=None, type=str)
+    parser.add_argument('-save', '--save_path', default=None, type=str)
+    parser.add_argument('--max_steps', default=100000, type=int)
+    parser.add_argument('--warm_up_steps', default=None, type=int)
+    parser.add_argument('--save_checkpoint_steps', default=10000, type=int)
+    parser.add_argument('--valid_steps', default=10000, type=int)
+    parser.add_argument('--log_steps', default=100, type=int, help='train log every xx steps')
+    parser.add_argument('--test_log_steps', default=1000, type=int, help='valid/test log every xx steps')
+    parser.add_argument('--nentity', type=int, default=0, help='DO NOT MANUALLY SET')
+    parser.add_argument('--nrelation', type=int, default=0, help='DO NOT MANUALLY SET')
+    return parser.parse_args(args)
+
+
+def override_config(args):
+    '''Restore the model/data configuration of -init (run.py:75-90).'''
+    with open(os.path.join(args.init_checkpoint, 'config.json'), 'r') as fjson:
+        argparse_dict = json.load(fjson)
+    args.countries = argparse_dict['countries']
+    if args.data_path is None:
+        args.data_path = argparse_dict['data_path']
+    args.model = argparse_dict['model']
+    args.double_entity_embedding = argparse_dict['double_entity_embedding']
+    args.double_relation_embedding = argparse_dict['double_relation_embedding']
+    args.hidden_dim = argparse_dict['hidden_dim']
+    args.test_batch_size = argparse_dict['test_batch_size']
+
+
+def _json_args(args):
+    return {k: v for k, v in vars(args).items() if not k.startswith('dp_')}
+
+
+def save_model(model, optimizer, save_variable_list, args):
+    '''config.json + checkpoint + entity/relation_embedding.npy (run.py:93-120).'''
+    with open(os.path.join(args.save_path, 'config.json'), 'w') as fjson:
+        json.dump(_json_args(args), fjson)
+    torch.save({
+        **save_variable_list,
+        'model_state_dict': model.state_dict(),
+        'optimizer_state_dict': optimizer.state_dict()},
+        os.path.join(args.save_path, 'checkpoint')
+    )
+    np.save(os.path.join(args.save_path, 'entity_embedding'), model.entity_embedding.detach().cpu().numpy())
+    np.save(os.path.join(args.save_path, 'relation_embedding'), model.relation_embedding.detach().cpu().numpy())
+
+
+def read_triple(file_path, entity2id, relation2id):
+    '''Triples mapped to ids (run.py:123-132).'''
+    triples = []
+    with open(file_path) as fin:
+        for line in fin:
+            h, r, t = line.strip().split('\t')
+            triples.append((entity2id[h], relation2id[r], entity2id[t]))
+    return triples
+
+
+def read_dict(file_path):
+    out = dict()
+    with open(file_path) as fin:
+        for line in fin:
+            eid, name = line.strip().split('\t')
+            out[name] = int(eid)
+    return out
+
+
+def set_logger(args, rank=0):
+    '''Log to <save_path>/train.log (or test.log) and the console (run.py:135-156).'''
+    if rank != 0:
+        logging.basicConfig(level=logging.WARNING)
+        return
+    if args.do_train:
+        log_file = os.path.join(args.save_path or args.init_checkpoint, 'train.log')
+    else:
+        log_file = os.path.join(args.save_path or args.init_checkpoint, 'test.log')
+    for h in list(logging.getLogger('').handlers):
+        logging.getLogger('').removeHandler(h)
+    logging.basicConfig(format='%(asctime)s %(levelname)-8s %(message)s', level=logging.INFO,
+                        datefmt='%Y-%m-%d %H:%M:%S', filename=log_file, filemode='w')
+    console = logging.StreamHandler()
+    console.setLevel(logging.INFO)
+    console.setFormatter(logging.Formatter('%(asctime)s %(levelname)-8s %(message)s'))
+    logging.getLogger('').addHandler(console)
+
+
+def log_metrics(mode, step, metrics):
+    for metric in metrics:
+        logging.info('%s %s at step %d: %f' % (mode, metric, step, metrics[metric]))
+
+
+def _init_distributed(args):
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    args.dp_group = None
+    if world <= 1:
+        return 0
+    import torch.distributed as dist
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    torch.cuda.set_device(local)
+    if not dist.is_initialized():
+        dist.init_process_group('nccl' if torch.cuda.is_available() else 'gloo')
+    args.dp_group = dist.group.WORLD
+    return dist.get_rank()
+
+
+def main(args):
+    if (not args.do_train) and (not args.do_valid) and (not args.do_test):
+        raise ValueError('one of train/val/test mode must be choosed.')
+    if args.init_checkpoint:
+        override_config(args)
+    elif args.data_path is None:
+        raise ValueError('one of init_checkpoint/data_path must be choosed.')
+    if args.do_train and args.save_path is None:
+        raise ValueError('Where do you want to save your trained model?')
+    rank = _init_distributed(args)
+    if args.save_path and not os.path.exists(args.save_path) and rank == 0:
+        os.makedirs(args.save_path)
+    set_logger(args, rank)
+
+    if not torch.cuda.is_available():
+        raise RuntimeError('knowledgegraphembedding_amd computes on MI355X (ROCm) only; no GPU is visible')
+    if not args.cuda:
+        logging.info('--cuda implied: knowledgegraphembedding_amd has no CPU compute path')
+        args.cuda = True
+
+    entity2id = read_dict(os.path.join(args.data_path, 'entities.dict'))
+    relation2id = read_dict(os.path.join(args.data_path, 'relations.dict'))
+    if args.countries:
+        regions = list()
+        with open(os.path.join(args.data_path, 'regions.list')) as fin:
+            for line in fin:
+                regions.append(entity2id[line.strip()])
+        args.regions = regions
+
+    nentity, nrelation = len(entity2id), len(relation2id)
+    args.nentity, args.nrelation = nentity, nrelation
+    logging.info('Model: %s' % args.model)
+    logging.info('Data Path: %s' % args.data_path)
+    logging.info('#entity: %d' % nentity)
+    logging.info('#relation: %d' % nrelation)
+
+    train_triples = read_triple(os.path.join(args.data_path, 'train.txt'), entity2id, relation2id)
+    logging.info('#train: %d' % len(train_triples))
+    valid_triples = read_triple(os.path.join(args.data_path, 'valid.txt'), entity2id, relation2id)
+    logging.info('#valid: %d' % len(valid_triples))
+    test_triples = read_triple(os.path.join(args.data_path, 'test.txt'), entity2id, relation2id)
+    logging.info('#test: %d' % len(test_triples))
+    all_true_triples = train_triples + valid_triples + test_triples
+
+    kge_model = KGEModel(model_name=args.model, nentity=nentity, nrelation=nrelation, hidden_dim=args.hidden_dim,
+                         gamma=args.gamma, double_entity_embedding=args.double_entity_embedding,
+                         double_relation_embedding=args.double_relation_embedding)
+    logging.info('Model Parameter Configuration:')
+    for name, param in kge_model.named_parameters():
+        logging.info('Parameter %s: %s, require_grad = %s' % (name, str(param.size()), str(param.requires_grad)))
+    kge_model = kge_model.cuda()
+    if args.dp_group is not None:
+        # replicas start from rank 0's initialisation
+        import torch.distributed as dist
+        for p in kge_model.parameters():
+            dist.broadcast(p.data, src=0)
+
+    if args.do_train:
+        train_dataloader_head = DataLoader(
+            TrainDataset(train_triples, nentity, nrelation, args.negative_sample_size, 'head-batch'),
+            batch_size=args.batch_size, shuffle=True, num_workers=max(1, args.cpu_num // 2),
+            collate_fn=TrainDataset.collate_fn)
+        train_dataloader_tail = DataLoader(
+            TrainDataset(train_triples, nentity, nrelation, args.negative_sample_size, 'tail-batch'),
+            batch_size=args.batch_size, shuffle=True, num_workers=max(1, args.cpu_num // 2),
+            collate_fn=TrainDataset.collate_fn)
+        train_iterator = BidirectionalOneShotIterator(train_dataloader_head, train_dataloader_tail)
+        current_learning_rate = args.learning_rate
+        optimizer = KGEAdam(filter(lambda p: p.requires_grad, kge_model.parameters()), lr=current_learning_rate)
+        warm_up_steps = args.warm_up_steps if args.warm_up_steps else args.max_steps // 2
+
+    if args.init_checkpoint:
+        logging.info('Loading checkpoint %s...' % args.init_checkpoint)
+        checkpoint = torch.load(os.path.join(args.init_checkpoint, 'checkpoint'), map_location='cpu',
+                                weights_only=True)
+        init_step = checkpoint['step']
+        kge_model.load_state_dict(checkpoint['model_state_dict'])
+        if args.do_train:
+            current_learning_rate = checkpoint['current_learning_rate']
+            warm_up_steps = checkpoint['warm_up_steps']
+            optimizer.load_state_dict(checkpoint['optimizer_state_dict'])
+    else:
+        logging.info('Ramdomly Initializing %s Model...' % args.model)
+        init_step = 0
+
+    step = init_step
+    logging.info('Start Training...')
+    logging.info('init_step = %d' % init_step)
+    logging.info('batch_size = %d' % args.batch_size)
+    logging.info('negative_adversarial_sampling = %d' % args.negative_adversarial_sampling)
+    logging.info('hidden_dim = %d' % args.hidden_dim)
+    logging.info('gamma = %f' % args.gamma)
+    logging.info('negative_adversarial_sampling = %s' % str(args.negative_adversarial_sampling))
+    if args.negative_adversarial_sampling:
+        logging.info('adversarial_temperature = %f' % args.adversarial_temperature)
+
+    if args.do_train:
+        logging.info('learning_rate = %d' % current_learning_rate)
+        training_logs = []
+        for step in range(init_step, args.max_steps):
+            log = kge_model.train_step(kge_model, optimizer, train_iterator, args)
+            training_logs.append(log)
+            if step >= warm_up_steps:
+                current_learning_rate = current_learning_rate / 10
+                logging.info('Change learning_rate to %f at step %d' % (current_learning_rate, step))
+                optimizer = KGEAdam(filter(lambda p: p.requires_grad, kge_model.parameters()),
+                                    lr=current_learning_rate)
+                warm_up_steps = warm_up_steps * 3
+            if step % args.save_checkpoint_steps == 0 and rank == 0:
+                save_model(kge_model, optimizer, {'step': step, 'current_learning_rate': current_learning_rate,
+                                                  'warm_up_steps': warm_up_steps}, args)
+            if step % args.log_steps == 0:
+                metrics = {}
+                for metric in training_logs[0].keys():
+                    metrics[metric] = sum([log[metric] for log in training_logs]) / len(training_logs)
+                log_metrics('Training average', step, metrics)
+                training_logs = []
+            if args.do_valid and step % args.valid_steps == 0 and rank == 0:
+                logging.info('Evaluating on Valid Dataset...')
+                metrics = kge_model.test_step(kge_model, valid_triples, all_true_triples, args)
+                log_metrics('Valid', step, metrics)
+        if rank == 0:
+            save_model(kge_model, optimizer, {'step': step, 'current_learning_rate': current_learning_rate,
+                                              'warm_up_steps': warm_up_steps}, args)
+
+    if rank != 0:
+        return
+    if args.do_valid:
+        logging.info('Evaluating on Valid Dataset...')
+        metrics = kge_model.test_step(kge_model, valid_triples, all_true_triples, args)
+        log_metrics('Valid', step, metrics)
+    if args.do_test:
+        logging.info('Evaluating on Test Dataset...')
+        metrics = kge_model.test_step(kge_model, test_triples, all_true_triples, args)
+        log_metrics('Test', step, metrics)
+    if args.evaluate_train:
+        logging.info('Evaluating on Training Dataset...')
+        metrics = kge_model.test_step(kge_model, train_triples, all_true_triples, args)
+        log_metrics('Test', step, metrics)
+
+
+if __name__ == '__main__':
+    main(parse_args())

@@ -1,0 +1,203 @@
+"""CPU oracle for the KGE hot path — TEST INFRASTRUCTURE, NOT PRODUCT CODE.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may
+import this module, and only as the checker (or the timed CPU baseline) —
+never as a compute path of knowledgegraphembedding_amd.
+
+It restates the reference's algorithm (kahrabian/KnowledgeGraphEmbedding,
+codes/model.py + codes/dataloader.py) as the same ATen op chain on CPU fp32
+tensors, so on one machine it reproduces the reference's floats; integer
+work (filters, ranks) is numpy.  Pinning: tests/test_oracle_golden.py checks
+every function below against tests/golden/*.npz, generated in the build
+container by importing the reference itself (tests/golden/make_golden.py).
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+PI = 3.14159265358979323846        # model.py:202
+PI_PROTATE = 3.14159262358979323846  # model.py:232 (typo kept: it is the reference's behaviour)
+
+
+# --------------------------------------------------------------- gather
+def gather(ent: torch.Tensor, rel: torch.Tensor, sample, mode: str):
+    """Row gathers of KGEModel.forward (model.py:83-149) → (head, relation, tail)."""
+    sel = lambda table, idx: torch.index_select(table, 0, idx)  # noqa: E731
+    if mode == 'single':
+        s = sample
+        return sel(ent, s[:, 0]).unsqueeze(1), sel(rel, s[:, 1]).unsqueeze(1), sel(ent, s[:, 2]).unsqueeze(1)
+    if mode == 'head-batch':
+        pos, neg = sample
+        b, n = neg.shape
+        return (sel(ent, neg.reshape(-1)).view(b, n, -1), sel(rel, pos[:, 1]).unsqueeze(1),
+                sel(ent, pos[:, 2]).unsqueeze(1))
+    if mode == 'tail-batch':
+        pos, neg = sample
+        b, n = neg.shape
+        return (sel(ent, pos[:, 0]).unsqueeze(1), sel(rel, pos[:, 1]).unsqueeze(1),
+                sel(ent, neg.reshape(-1)).view(b, n, -1))
+    raise ValueError('mode %s not supported' % mode)
+
+
+# --------------------------------------------------------------- scores
+def _transe(h, r, t, mode, gamma, erange, modulus):  # model.py:166-173
+    x = h + (r - t) if mode == 'head-batch' else (h + r) - t
+    return gamma - torch.norm(x, p=1, dim=2)
+
+
+def _distmult(h, r, t, mode, gamma, erange, modulus):  # model.py:175-182
+    x = h * (r * t) if mode == 'head-batch' else (h * r) * t
+    return x.sum(dim=2)
+
+
+def _complex(h, r, t, mode, gamma, erange, modulus):  # model.py:184-199
+    hr, hi = torch.chunk(h, 2, dim=2)
+    rr, ri = torch.chunk(r, 2, dim=2)
+    tr, ti = torch.chunk(t, 2, dim=2)
+    if mode == 'head-batch':
+        a = rr * tr + ri * ti
+        b = rr * ti - ri * tr
+        x = hr * a + hi * b
+    else:
+        a = hr * rr - hi * ri
+        b = hr * ri + hi * rr
+        x = a * tr + b * ti
+    return x.sum(dim=2)
+
+
+def _rotate(h, r, t, mode, gamma, erange, modulus):  # model.py:201-229
+    hr, hi = torch.chunk(h, 2, dim=2)
+    tr, ti = torch.chunk(t, 2, dim=2)
+    phase = r / (erange / PI)
+    c, s = torch.cos(phase), torch.sin(phase)
+    if mode == 'head-batch':
+        a = (c * tr + s * ti) - hr
+        b = (c * ti - s * tr) - hi
+    else:
+        a = (hr * c - hi * s) - tr
+        b = (hr * s + hi * c) - ti
+    mod = torch.stack([a, b], dim=0).norm(dim=0)
+    return gamma - mod.sum(dim=2)
+
+
+def _protate(h, r, t, mode, gamma, erange, modulus):  # model.py:231-249
+    k = erange / PI_PROTATE
+    ph, pr, pt = h / k, r / k, t / k
+    x = ph + (pr - pt) if mode == 'head-batch' else (ph + pr) - pt
+    return gamma - torch.abs(torch.sin(x)).sum(dim=2) * modulus
+
+
+SCORE_FNS = {'TransE': _transe, 'DistMult': _distmult, 'ComplEx': _complex, 'RotatE': _rotate,
+             'pRotatE': _protate}
+
+
+def forward(name, ent, rel, modulus, sample, mode, gamma: float, erange: float):
+    """KGEModel.forward (model.py:72-164): [B, n] scores."""
+    h, r, t = gather(ent, rel, sample, mode)
+    return SCORE_FNS[name](h, r, t, mode, gamma, erange, modulus)
+
+
+# --------------------------------------------------------------- training
+def train_grads(name, ent, rel, modulus, pos, neg, w, mode, *, adversarial: bool, temperature: float,
+                uni_weight: bool, regularization: float, gamma: float, erange: float):
+    """train_step up to loss.backward() (model.py:268-301).
+
+    Returns ({'positive_sample_loss', 'negative_sample_loss', 'loss'[, 'regularization']},
+             grad_entity, grad_relation, grad_modulus-or-None) — dense gradients.
+    """
+    E = ent.detach().clone().requires_grad_(True)
+    R = rel.detach().clone().requires_grad_(True)
+    Mo = modulus.detach().clone().requires_grad_(True) if modulus is not None else None
+    neg_s = forward(name, E, R, Mo, (pos, neg), mode, gamma, erange)
+    if adversarial:
+        wts = F.softmax(neg_s * temperature, dim=1).detach()
+        neg_term = (wts * F.logsigmoid(-neg_s)).sum(dim=1)
+    else:
+        neg_term = F.logsigmoid(-neg_s).mean(dim=1)
+    pos_term = F.logsigmoid(forward(name, E, R, Mo, pos, 'single', gamma, erange)).squeeze(dim=1)
+    if uni_weight:
+        p_loss, n_loss = -pos_term.mean(), -neg_term.mean()
+    else:
+        p_loss = -(w * pos_term).sum() / w.sum()
+        n_loss = -(w * neg_term).sum() / w.sum()
+    loss = (p_loss + n_loss) / 2
+    out = {}
+    if regularization != 0.0:
+        reg = regularization * (E.norm(p=3) ** 3 + R.norm(p=3).norm(p=3) ** 3)
+        loss = loss + reg
+        out['regularization'] = reg.item()
+    loss.backward()
+    out.update({'positive_sample_loss': p_loss.item(), 'negative_sample_loss': n_loss.item(), 'loss': loss.item()})
+    return out, E.grad, R.grad, (Mo.grad if Mo is not None else None)
+
+
+def adam_steps(params, grads_per_step, lr: float):
+    """torch.optim.Adam(params, lr) stepped once per entry of grads_per_step
+    (run.py:266-269, model.py:303); returns (params, state tensors)."""
+    ps = [p.detach().clone().requires_grad_(True) for p in params]
+    opt = torch.optim.Adam(ps, lr=lr)
+    for grads in grads_per_step:
+        opt.zero_grad()
+        for p, g in zip(ps, grads):
+            p.grad = g.clone()
+        opt.step()
+    states = [(opt.state[p]['exp_avg'].clone(), opt.state[p]['exp_avg_sq'].clone()) for p in ps]
+    return [p.detach() for p in ps], states
+
+
+# --------------------------------------------------------------- ranking
+def filtered_candidates(triple, all_true_set, nentity: int, mode: str):
+    """TestDataset.__getitem__ (dataloader.py:134-154): (negative_sample [E], filter_bias [E])."""
+    h, r, t = triple
+    cand = np.arange(nentity, dtype=np.int64)
+    bias = np.zeros(nentity, dtype=np.float32)
+    for e in range(nentity):
+        key = (e, r, t) if mode == 'head-batch' else (h, r, e)
+        if key in all_true_set:
+            cand[e] = h if mode == 'head-batch' else t
+            bias[e] = -1.0
+    true_id = h if mode == 'head-batch' else t
+    cand[true_id] = true_id
+    bias[true_id] = 0.0
+    return cand, bias
+
+
+def filtered_ranks(name, ent, rel, modulus, triples, all_true_triples, mode, gamma: float, erange: float):
+    """test_step's rank per query (model.py:383-418), plus diagnostics.
+
+    Returns dict of numpy arrays:
+      rank_argsort  1 + position of the true entity in argsort(desc) — the reference's number
+      rank_count    1 + #{unfiltered e != true : s_e > s_true} (strict count, tie-free definition)
+      ties          #{unfiltered e != true : s_e == s_true}
+      margin64      min over unfiltered e != true of |s_e - s_true| recomputed in float64
+    """
+    all_true_set = set(map(tuple, np.asarray(all_true_triples).tolist()))
+    E = ent.shape[0]
+    out = {k: [] for k in ('rank_argsort', 'rank_count', 'ties', 'margin64')}
+    for tr in np.asarray(triples, dtype=np.int64).tolist():
+        cand, bias = filtered_candidates(tr, all_true_set, E, mode)
+        pos = torch.tensor([tr], dtype=torch.int64)
+        negt = torch.from_numpy(cand).view(1, -1)
+        s = forward(name, ent, rel, modulus, (pos, negt), mode, gamma, erange)
+        s = s + torch.from_numpy(bias).view(1, -1)
+        arg = torch.argsort(s, dim=1, descending=True)
+        true_id = tr[0] if mode == 'head-batch' else tr[2]
+        out['rank_argsort'].append(1 + int((arg[0] == true_id).nonzero().item()))
+        s0 = s[0].numpy()
+        keep = (bias == 0) & (np.arange(E) != true_id)
+        st = s0[true_id]
+        out['rank_count'].append(1 + int((s0[keep] > st).sum()))
+        out['ties'].append(int((s0[keep] == st).sum()))
+        s64 = forward(name, ent.double(), rel.double(), None if modulus is None else modulus.double(), (pos, negt),
+                      mode, gamma, erange)[0].numpy()
+        out['margin64'].append(float(np.min(np.abs(s64[keep] - s64[true_id]))) if keep.any() else np.inf)
+    return {k: np.asarray(v) for k, v in out.items()}
+
+
+def metrics_from_ranks(ranks):
+    """MRR / MR / HITS@k averaged the way model.py:412-427 averages its log dicts."""
+    logs = [{'MRR': 1.0 / r, 'MR': float(r), 'HITS@1': 1.0 if r <= 1 else 0.0, 'HITS@3': 1.0 if r <= 3 else 0.0,
+             'HITS@10': 1.0 if r <= 10 else 0.0} for r in np.asarray(ranks).tolist()]
+    return {k: sum(l[k] for l in logs) / len(logs) for k in logs[0]}

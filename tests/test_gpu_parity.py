@@ -1,0 +1,319 @@
+"""HIP path vs the reference's golden vectors and vs the CPU oracle (GPU box).
+
+Tolerances (north star):
+  scores / losses:  |Δ| ≤ 1e-4 · max(|s_ref|, 1)
+  gradients:        |Δ| ≤ 1e-4 · max|g_ref| + 1e-4 · |g_ref|  (fp32 sums in another order)
+  ranks:            bit-exact on every query whose fp64 margin exceeds 1e-4·max(|s|,1);
+                    tie / near-tie queries are reported, and must stay within [count, count+ties]
+"""
+from argparse import Namespace
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import dims, score_tol, synth_tables
+from knowledgegraphembedding_amd import KGEAdam, KGEModel, synth
+from knowledgegraphembedding_amd import ops
+from oracle import kge_oracle as O
+
+pytestmark = pytest.mark.gpu
+NAMES = ["TransE", "DistMult", "ComplEx", "RotatE", "pRotatE"]
+DEV = torch.device("cuda", 0)
+
+
+def build_model(name, E, R, d, gamma, seed):
+    de, dr = {"TransE": (0, 0), "DistMult": (0, 0), "ComplEx": (1, 1), "RotatE": (1, 0), "pRotatE": (0, 0)}[name]
+    m = KGEModel(name, E, R, d, gamma, bool(de), bool(dr))
+    ent, rel, mod, rng = synth_tables(name, E, R, d, gamma, seed)
+    with torch.no_grad():
+        m.entity_embedding.copy_(torch.from_numpy(ent))
+        m.relation_embedding.copy_(torch.from_numpy(rel))
+    return m.to(DEV), ent, rel, mod, rng
+
+
+def assert_close_grad(got, ref, msg=""):
+    tol = 1e-4 * np.abs(ref).max() + 1e-4 * np.abs(ref) + 1e-12
+    bad = np.abs(got - ref) > tol
+    assert not bad.any(), f"{msg}: {bad.sum()} elements off, max |Δ| {np.abs(got - ref).max():.3e}"
+
+
+# ------------------------------------------------------------------ scores
+@pytest.mark.parametrize("tag,E,R,d,B,n,gamma,seed", [("small", 64, 8, 16, 4, 8, 12.0, 11),
+                                                       ("d1000", 128, 16, 1000, 8, 16, 24.0, 12)])
+@pytest.mark.parametrize("name", NAMES)
+def test_scores_vs_golden(g_scores, tag, E, R, d, B, n, gamma, seed, name):
+    m, *_ = build_model(name, E, R, d, gamma, seed)
+    pos, neg, _ = synth.kge_batch(seed, B, n, E, R)
+    P, N = torch.from_numpy(pos).to(DEV), torch.from_numpy(neg).to(DEV)
+    with torch.no_grad():
+        for mode in ("single", "head-batch", "tail-batch"):
+            s = (m(P) if mode == "single" else m((P, N), mode)).cpu().numpy()
+            ref = g_scores[f"{tag}/{name}/{mode}"]
+            assert s.shape == ref.shape
+            assert np.all(np.abs(s - ref) <= score_tol(ref)), f"{name} {mode} max|Δ| {np.abs(s - ref).max()}"
+
+
+@pytest.mark.parametrize("name", NAMES)
+def test_scores_vs_oracle_odd_dims(name):
+    # d not a multiple of 4 → scalar-slot kernels (VEC=1); n not a multiple of the unroll
+    E, R, d, B, n, gamma = 97, 7, 13 if name not in ("ComplEx", "RotatE") else 14, 5, 7, 6.0
+    m, ent, rel, mod, rng = build_model(name, E, R, d, gamma, 3)
+    pos, neg, _ = synth.kge_batch(5, B, n, E, R)
+    P, N = torch.from_numpy(pos), torch.from_numpy(neg)
+    g = torch.Tensor([gamma]).item()
+    modt = None if mod is None else torch.from_numpy(mod)
+    with torch.no_grad():
+        for mode in ("single", "head-batch", "tail-batch"):
+            ref = O.forward(name, torch.from_numpy(ent), torch.from_numpy(rel), modt,
+                            P if mode == "single" else (P, N), mode, g, rng).numpy()
+            s = (m(P.to(DEV)) if mode == "single" else m((P.to(DEV), N.to(DEV)), mode)).cpu().numpy()
+            assert np.all(np.abs(s - ref) <= score_tol(ref)), f"{name} {mode}"
+
+
+# ------------------------------------------------------------------ training
+def _train_case(g_train, golden_info, ci):
+    ti = golden_info["train"]
+    case = ti["cases"][ci]
+    name = case["model"]
+    m, ent, rel, mod, rng = build_model(name, ti["E"], ti["R"], ti["d"], ti["gamma"], ti["seed"])
+    pos, neg, w = synth.kge_batch(ti["seed"] + ci, ti["B"], ti["n"], ti["E"], ti["R"])
+    args = Namespace(cuda=True, negative_adversarial_sampling=case["adversarial"],
+                     adversarial_temperature=ti["adversarial_temperature"], uni_weight=case["uni_weight"],
+                     regularization=case["regularization"])
+    batch = (torch.from_numpy(pos), torch.from_numpy(neg), torch.from_numpy(w), case["mode"])
+    return m, args, batch, case, ti
+
+
+def test_train_step_vs_golden(g_train, golden_info):
+    for ci in range(len(golden_info["train"]["cases"])):
+        m, args, batch, case, ti = _train_case(g_train, golden_info, ci)
+        opt = KGEAdam([p for p in m.parameters() if p.requires_grad], lr=ti["lr"])
+        grads = {}
+
+        class Rec:
+            def zero_grad(self):
+                opt.zero_grad()
+
+            def step(self):
+                if not grads:
+                    grads["e"] = m.entity_embedding.grad.detach().cpu().numpy().copy()
+                    grads["r"] = m.relation_embedding.grad.detach().cpu().numpy().copy()
+                    if case["model"] == "pRotatE":
+                        grads["m"] = m.modulus.grad.detach().cpu().numpy().copy()
+                opt.step()
+
+        log = KGEModel.train_step(m, Rec(), iter([batch]), args)
+        log2 = KGEModel.train_step(m, Rec(), iter([batch]), args)
+        ref = g_train[f"{ci}/log"]
+        got = np.array([log["positive_sample_loss"], log["negative_sample_loss"], log["loss"],
+                        log.get("regularization", 0.0)])
+        assert np.all(np.abs(got - ref) <= score_tol(ref)), f"{case} log {got} vs {ref}"
+        assert ("regularization" in log) == (case["regularization"] != 0.0)
+        assert_close_grad(grads["e"], g_train[f"{ci}/grad_entity"], f"{case} grad_entity")
+        assert_close_grad(grads["r"], g_train[f"{ci}/grad_relation"], f"{case} grad_relation")
+        if case["model"] == "pRotatE":
+            assert_close_grad(grads["m"], g_train[f"{ci}/grad_modulus"], f"{case} grad_modulus")
+        ref2 = g_train[f"{ci}/log2"]
+        got2 = np.array([log2["positive_sample_loss"], log2["negative_sample_loss"], log2["loss"],
+                         log2.get("regularization", 0.0)])
+        assert np.all(np.abs(got2 - ref2) <= score_tol(ref2)), f"{case} step-2 log"
+        p2 = m.entity_embedding.detach().cpu().numpy()
+        r2 = g_train[f"{ci}/param2_entity"]
+        # two Adam steps of lr 0.01 on |p| ~ 1: tolerance scaled to the update size
+        assert np.abs(p2 - r2).max() <= 2e-4 * 0.01 * 2 + 1e-6, f"{case} params after 2 steps"
+
+
+@pytest.mark.parametrize("name", NAMES)
+@pytest.mark.parametrize("mode", ["head-batch", "tail-batch"])
+def test_train_grads_vs_oracle_realistic(name, mode):
+    """d=1000-class rows, n=64: fused kernel vs the oracle's autograd."""
+    E, R, d, B, n, gamma = 600, 20, 200 if name != "DistMult" else 400, 16, 64, 24.0
+    m, ent, rel, mod, rng = build_model(name, E, R, d, gamma, 8)
+    pos, neg, w = synth.kge_batch(9, B, n, E, R)
+    g = torch.Tensor([gamma]).item()
+    for adv in (True, False):
+        args = Namespace(negative_adversarial_sampling=adv, adversarial_temperature=1.0, uni_weight=False,
+                         regularization=0.0)
+        losses = m.compute_train_grads(torch.from_numpy(pos).to(DEV), torch.from_numpy(neg).to(DEV),
+                                       torch.from_numpy(w).to(DEV), mode, args).cpu().numpy()
+        ops.raise_on_device_error(DEV)
+        log, ge, gr, gm = O.train_grads(name, torch.from_numpy(ent), torch.from_numpy(rel),
+                                        None if mod is None else torch.from_numpy(mod), torch.from_numpy(pos),
+                                        torch.from_numpy(neg), torch.from_numpy(w), mode, adversarial=adv,
+                                        temperature=1.0, uni_weight=False, regularization=0.0, gamma=g, erange=rng)
+        ref = np.array([log["positive_sample_loss"], log["negative_sample_loss"], log["loss"]])
+        assert np.all(np.abs(losses[:3] - ref) <= score_tol(ref))
+        assert_close_grad(m.entity_embedding.grad.cpu().numpy(), ge.numpy(), f"{name} {mode} adv={adv} ent")
+        assert_close_grad(m.relation_embedding.grad.cpu().numpy(), gr.numpy(), f"{name} {mode} adv={adv} rel")
+        if gm is not None:
+            assert_close_grad(m.modulus.grad.cpu().numpy(), gm.numpy(), f"{name} modulus")
+
+
+def test_train_grads_deterministic():
+    m, *_ = build_model("RotatE", 3000, 50, 250, 24.0, 4)
+    pos, neg, w = synth.kge_batch(4, 64, 128, 3000, 50)
+    args = Namespace(negative_adversarial_sampling=True, adversarial_temperature=1.0, uni_weight=False,
+                     regularization=0.0)
+    outs = []
+    for _ in range(2):
+        losses = m.compute_train_grads(torch.from_numpy(pos).to(DEV), torch.from_numpy(neg).to(DEV),
+                                       torch.from_numpy(w).to(DEV), "tail-batch", args)
+        outs.append((losses.cpu().clone(), m.entity_embedding.grad.cpu().clone(),
+                     m.relation_embedding.grad.cpu().clone()))
+    for a, b in zip(outs[0], outs[1]):
+        assert torch.equal(a, b)
+
+
+# ------------------------------------------------------------ forward autograd
+@pytest.mark.parametrize("name", NAMES)
+@pytest.mark.parametrize("mode", ["single", "head-batch", "tail-batch"])
+def test_forward_backward_vs_oracle(name, mode):
+    E, R, d, B, n, gamma = 80, 6, 24, 6, 10, 9.0
+    m, ent, rel, mod, rng = build_model(name, E, R, d, gamma, 13)
+    pos, neg, _ = synth.kge_batch(14, B, n, E, R)
+    n_eff = 1 if mode == "single" else n
+    gout = synth.uniform(15, (B, n_eff), -1.0, 1.0)
+    P, N = torch.from_numpy(pos), torch.from_numpy(neg)
+    s = m(P.to(DEV)) if mode == "single" else m((P.to(DEV), N.to(DEV)), mode)
+    s.backward(torch.from_numpy(gout).to(DEV))
+    E_ = torch.from_numpy(ent).requires_grad_(True)
+    R_ = torch.from_numpy(rel).requires_grad_(True)
+    M_ = torch.from_numpy(mod).requires_grad_(True) if mod is not None else None
+    ref = O.forward(name, E_, R_, M_, P if mode == "single" else (P, N), mode, torch.Tensor([gamma]).item(), rng)
+    ref.backward(torch.from_numpy(gout))
+    assert np.all(np.abs(s.detach().cpu().numpy() - ref.detach().numpy()) <= score_tol(ref.detach().numpy()))
+    assert_close_grad(m.entity_embedding.grad.cpu().numpy(), E_.grad.numpy(), f"{name} {mode} ent")
+    assert_close_grad(m.relation_embedding.grad.cpu().numpy(), R_.grad.numpy(), f"{name} {mode} rel")
+    if M_ is not None:
+        assert_close_grad(m.modulus.grad.cpu().numpy(), M_.grad.numpy(), f"{name} {mode} modulus")
+
+
+@pytest.mark.parametrize("name", NAMES)
+def test_plugin_methods(name):
+    """model.TransE(head, relation, tail, mode) on gathered rows == forward()."""
+    E, R, d, B, n = 50, 5, 16, 3, 7
+    m, ent, rel, mod, rng = build_model(name, E, R, d, 12.0, 21)
+    pos, neg, _ = synth.kge_batch(22, B, n, E, R)
+    P, N = torch.from_numpy(pos).to(DEV), torch.from_numpy(neg).to(DEV)
+    with torch.no_grad():
+        for mode in ("single", "head-batch", "tail-batch"):
+            h, r, t = O.gather(m.entity_embedding, m.relation_embedding, P if mode == "single" else (P, N), mode)
+            a = getattr(m, name)(h, r, t, mode)
+            b = m(P) if mode == "single" else m((P, N), mode)
+            torch.testing.assert_close(a, b, rtol=0, atol=0)
+
+
+def test_index_error():
+    m, *_ = build_model("RotatE", 30, 4, 8, 12.0, 1)
+    bad = torch.tensor([[0, 1, 99]], device=DEV)
+    with pytest.raises(IndexError):
+        m(bad)
+        ops.raise_on_device_error(DEV)
+
+
+# ------------------------------------------------------------------ Adam
+def test_kge_adam_matches_torch_adam():
+    torch.manual_seed(0)
+    p0 = torch.randn(1001, 37)
+    grads = [torch.randn(1001, 37) for _ in range(3)]
+    a = p0.clone().to(DEV).requires_grad_(True)
+    b = p0.clone().to(DEV).requires_grad_(True)
+    oa, ob = KGEAdam([a], lr=1e-3), torch.optim.Adam([b], lr=1e-3)
+    for g in grads:
+        a.grad, b.grad = g.to(DEV), g.to(DEV).clone()
+        oa.step()
+        ob.step()
+    torch.testing.assert_close(a, b, rtol=2e-6, atol=1e-7)
+    sd = oa.state_dict()
+    assert set(sd["state"][0]) == {"step", "exp_avg", "exp_avg_sq"}
+
+
+# ------------------------------------------------------------------ ranking
+def test_ranks_vs_golden(g_ranks, golden_info):
+    report = []
+    for kg in golden_info["ranks"]:
+        tag, E, R, d, seed = kg["tag"], kg["E"], kg["R"], kg["d"], kg["seed"]
+        all_true = g_ranks[f"{tag}/all_true"]
+        test = g_ranks[f"{tag}/test"]
+        for name in kg["models"]:
+            m, ent, rel, mod, rng = build_model(name, E, R, d, kg["gamma"], seed)
+            g = torch.Tensor([kg["gamma"]]).item()
+            for mode in ("head-batch", "tail-batch"):
+                ranks, ties = m.rank_queries(test, all_true, mode)
+                ref = g_ranks[f"{tag}/{name}/{mode}/rank"]
+                orc = O.filtered_ranks(name, torch.from_numpy(ent), torch.from_numpy(rel),
+                                       None if mod is None else torch.from_numpy(mod), test, all_true, mode, g, rng)
+                # margin in units of the score tolerance
+                s_scale = np.maximum(1.0, np.abs(orc["margin64"]))
+                clear = (orc["margin64"] > 1e-4 * s_scale * 10) & (ties == 0)
+                mism = (ranks != ref) & clear
+                assert not mism.any(), f"{tag} {name} {mode}: {np.nonzero(mism)[0]} {ranks[mism]} vs {ref[mism]}"
+                report.append((tag, name, mode, int(clear.sum()), int((~clear).sum()),
+                               int((ranks == ref).sum()), len(ref)))
+    print("rank parity (tag, model, mode, clear, ambiguous, exact, total):")
+    for r in report:
+        print("  ", r)
+
+
+def test_test_step_metrics_vs_golden(g_ranks, golden_info):
+    kg = golden_info["ranks"][0]
+    tag, E, R, d, seed = kg["tag"], kg["E"], kg["R"], kg["d"], kg["seed"]
+    all_true = [tuple(x) for x in g_ranks[f"{tag}/all_true"].tolist()]
+    test = [tuple(x) for x in g_ranks[f"{tag}/test"].tolist()]
+    for name in kg["models"]:
+        m, *_ = build_model(name, E, R, d, kg["gamma"], seed)
+        args = Namespace(countries=False, nentity=E, nrelation=R, test_batch_size=4, cpu_num=2, test_log_steps=1000,
+                         cuda=True)
+        met = KGEModel.test_step(m, test, all_true, args)
+        got = np.array([met[k] for k in golden_info["metric_order"]])
+        ref = g_ranks[f"{tag}/{name}/metrics"]
+        np.testing.assert_allclose(got, ref, rtol=0, atol=1e-12, err_msg=name)
+
+
+def test_countries_auc_pr(g_countries, golden_info):
+    ci = golden_info["countries"]
+    m, *_ = build_model("TransE", ci["nentity"], ci["nrelation"], ci["d"], ci["gamma"], ci["seed"])
+    args = Namespace(countries=True, regions=g_countries["regions"].tolist(), cuda=True)
+    test = [tuple(x) for x in g_countries["test"].tolist()]
+    met = KGEModel.test_step(m, test, [], args)
+    assert abs(met["auc_pr"] - g_countries["auc_pr"][0]) < 1e-6
+
+
+# ------------------------------------------------------------- full size
+def test_config2_full_size_properties():
+    """BASELINE config 2 shape (RotatE FB15k d=1000 b=1024 n=256 -adv): finite,
+    deterministic, and sampled rows equal to the oracle."""
+    E, R, d, B, n, gamma = 14951, 1345, 1000, 1024, 256, 24.0
+    m, ent, rel, mod, rng = build_model("RotatE", E, R, d, gamma, 0)
+    pos, neg, w = synth.kge_batch(1, B, n, E, R)
+    args = Namespace(negative_adversarial_sampling=True, adversarial_temperature=1.0, uni_weight=False,
+                     regularization=0.0)
+    res = []
+    for _ in range(2):
+        losses = m.compute_train_grads(torch.from_numpy(pos).to(DEV), torch.from_numpy(neg).to(DEV),
+                                       torch.from_numpy(w).to(DEV), "tail-batch", args)
+        res.append((losses.cpu().clone(), m.entity_embedding.grad.clone()))
+    ops.raise_on_device_error(DEV)
+    assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])
+    assert torch.isfinite(res[0][1]).all()
+    # scores of 8 sampled rows vs the oracle
+    rows = [0, 1, 100, 511, 512, 777, 1000, 1023]
+    P = torch.from_numpy(pos[rows])
+    N = torch.from_numpy(neg[rows])
+    with torch.no_grad():
+        s = m((P.to(DEV), N.to(DEV)), "tail-batch").cpu().numpy()
+    ref = O.forward("RotatE", torch.from_numpy(ent), torch.from_numpy(rel), None, (P, N), "tail-batch",
+                    torch.Tensor([gamma]).item(), rng).numpy()
+    assert np.all(np.abs(s - ref) <= score_tol(ref))
+    # gradient of the full batch equals the sum of per-half-batch gradients (linearity), both normalised by Σw
+    wsum = torch.tensor([float(w.sum(dtype=np.float32))], device=DEV)
+    acc = None
+    for lo, hi in ((0, 512), (512, 1024)):
+        m.compute_train_grads(torch.from_numpy(pos[lo:hi]).to(DEV), torch.from_numpy(neg[lo:hi]).to(DEV),
+                              torch.from_numpy(w[lo:hi]).to(DEV), "tail-batch", args, weight_sum=wsum)
+        g = m.entity_embedding.grad.clone()
+        acc = g if acc is None else acc + g
+    full = res[0][1]
+    tol = 1e-4 * full.abs().max() + 1e-4 * full.abs()
+    assert ((acc - full).abs() <= tol).all()
