@@ -155,17 +155,17 @@ def main():
     if group is not None:
         dist.barrier()
     dt = time.perf_counter() - t0
-    stage = (torch.zeros(5, dtype=torch.float32)).numpy()
+    stage = (torch.zeros(7, dtype=torch.float32)).numpy()
     import ctypes
-    _lib.check(lib.kge_stage_timer(2, stage.ctypes.data_as(ctypes.c_void_p), 5), "kge_stage_timer")
+    _lib.check(lib.kge_stage_timer(2, stage.ctypes.data_as(ctypes.c_void_p), 7), "kge_stage_timer")
     lib.kge_stage_timer(0, None, 0)
     if group is not None:
         t = torch.tensor([dt], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
 
-    calls = max(1.0, float(stage[4]))
-    row_ms = float(stage[0]) / calls
+    calls = max(1.0, float(stage[6]))
+    row_ms = float(stage[1]) / calls
     row_bytes = algorithmic_row_bytes(B, NNEG, 2 * D, D)
     achieved = row_bytes / (row_ms * 1e-3) / 1e9
     traffic = None
@@ -191,9 +191,10 @@ def main():
                    "entities": E, "relations": R, "hidden_dim": D, "batch_per_gpu": B, "global_batch": B * world,
                    "negatives": NNEG, "adversarial_temperature": TEMP, "gamma": GAMMA,
                    "parallelism": f"dp{world}"},
-        "stage_ms": {"row_pass": row_ms, "csr": float(stage[1]) / calls, "entity_pass": float(stage[2]) / calls,
-                     "relation_pass_finalize": float(stage[3]) / calls,
-                     "other_incl_adam_ms": dt / a.steps * 1e3 - float(stage[:4].sum()) / calls},
+        "stage_ms": {"build_q": float(stage[0]) / calls, "row_pass": row_ms, "row_epilogue": float(stage[2]) / calls,
+                     "csr": float(stage[3]) / calls, "entity_pass": float(stage[4]) / calls,
+                     "relation_pass_finalize": float(stage[5]) / calls,
+                     "other_incl_adam_ms": dt / a.steps * 1e3 - float(stage[:6].sum()) / calls},
         "roofline": {"bound": "hbm", "kernel": "k_row (fused negative scoring + self-adversarial loss)",
                      "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                      "traffic": traffic, "algorithmic_bytes_per_launch": row_bytes,

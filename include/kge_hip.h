@@ -176,15 +176,16 @@ int kge_rank_filtered(const kge_model_desc *m, int32_t mode, const int64_t *quer
 /*
  * Live stage timing for benchmarks (no reference counterpart): when enabled,
  * kge_train_step_grads records a hipEvent on its stream before and after each
- * stage — 0 row pass (fused scoring + loss), 1 occurrence CSR, 2 entity-major
- * gradient pass, 3 relation pass + loss finalisation.
+ * stage — 0 q build, 1 fused negative scoring + self-adversarial loss (the
+ * gather loop), 2 positive score + chain rule, 3 occurrence CSR, 4
+ * entity-major gradient pass, 5 relation pass + loss finalisation.
  *   command 1: enable and reset; 0: disable and reset;
  *   command 2: synchronise the recorded events and write the summed
- *              milliseconds per stage to stage_ms_out[0..3] and the number of
- *              timed calls to stage_ms_out[4] (n_out >= 5).
+ *              milliseconds per stage to stage_ms_out[0..5] and the number of
+ *              timed calls to stage_ms_out[6] (n_out >= 7).
  * Not graph-capturable while enabled.
  */
-#define KGE_TIMER_STAGES 4
+#define KGE_TIMER_STAGES 6
 int kge_stage_timer(int32_t command, float *stage_ms_out, int32_t n_out);
 
 #ifdef __cplusplus

@@ -1,6 +1,7 @@
 // kge_capi.hip — the extern "C" boundary declared in include/kge_hip.h.
 // Host-side argument checks, workspace carving and launch sequencing; no
 // allocation, no synchronisation (graph-capturable).
+#include <stdlib.h>
 #include <string.h>
 
 #include <vector>
@@ -83,7 +84,7 @@ struct Carver {
 };
 
 struct GradWs {
-  float *g, *q, *ent_contrib, *rel_contrib, *row_stats, *reg_partial, *wsum;
+  float *g, *q, *dq, *ent_contrib, *rel_contrib, *row_stats, *reg_partial, *wsum;
   int32_t *keys, *cnt, *off, *tmp, *occ;
 };
 
@@ -93,6 +94,7 @@ GradWs carve_grad(void* ws, const kge_model_desc* m, int64_t B, int64_t n, size_
   const int64_t Bn = B * n, N = Bn + 3 * B, nb = m->nentity + m->nrelation;
   w.g = c.take<float>(Bn);
   w.q = c.take<float>(B * (int64_t)m->entity_dim);
+  w.dq = c.take<float>(B * (int64_t)m->entity_dim);
   w.ent_contrib = c.take<float>(2 * B * (int64_t)m->entity_dim);
   w.rel_contrib = c.take<float>(B * (int64_t)m->relation_dim);
   w.row_stats = c.take<float>(B * 4);
@@ -129,6 +131,7 @@ struct StageTimer {
   }
 };
 StageTimer g_timer;
+void timer_mark(hipStream_t s) { g_timer.mark(s); }
 
 // Shared body of backward and train: row pass → CSR → entity pass → relation pass → finalise.
 int run_grad(const kge_model_desc* m, const Geom& geo, int mode, const int64_t* pos, const int64_t* neg,
@@ -137,9 +140,10 @@ int run_grad(const kge_model_desc* m, const Geom& geo, int mode, const int64_t* 
   const ModelOps& op = ops_for(m->model);
   const Consts c = consts_of(m);
   const int Le = m->entity_dim, Lr = m->relation_dim;
-  const size_t lds = sizeof(float) * (4 * (size_t)Le + (size_t)ra.n_lds + 32);
+  const size_t lds = sizeof(float) * (2 * 64 * (size_t)geo.ns * geo.vec + 2 * (size_t)Le + (size_t)ra.n_lds + 32);
   if (lds > 64 * 1024) return KGE_ERR_DIM;
   const bool timed = g_timer.on && ra.op == ROW_TRAIN;
+  ra.timer_mid = timed ? &timer_mark : nullptr;
   if (timed) g_timer.mark(s);
   int st = launch_status(op.row(mode, geo.vec, geo.ns, ra, lds, s));
   if (st) return st;
@@ -191,8 +195,13 @@ RowArgs row_args(const kge_model_desc* m, const Geom& geo, const int64_t* pos, c
   ra.pos = pos; ra.neg = neg; ra.neg_stride = ns;
   ra.B = B; ra.n = n; ra.E = m->nentity; ra.R = m->nrelation;
   ra.Le = m->entity_dim; ra.Lr = m->relation_dim; ra.eg = geo.eg; ra.c = consts_of(m);
-  ra.g_out = w.g; ra.q_out = w.q; ra.ent_contrib = w.ent_contrib; ra.rel_contrib = w.rel_contrib;
+  ra.g_out = w.g; ra.q_out = w.q; ra.dq_out = w.dq; ra.ent_contrib = w.ent_contrib; ra.rel_contrib = w.rel_contrib;
   ra.row_stats = w.row_stats; ra.err = err;
+  static const int pipe = [] {
+    const char* e = getenv("KGE_ROW_PIPE");
+    return e ? atoi(e) : 0;
+  }();
+  ra.pipe = pipe;
   return ra;
 }
 

@@ -92,7 +92,7 @@ __global__ __launch_bounds__(256) void k_csr_rank(CsrArgs a) {
 // order (+ 3λ r|r|), written densely.
 __global__ __launch_bounds__(256) void k_rel_rows(RelArgs a) {
   const int lane = threadIdx.x & 63;
-  const int64_t rr = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int64_t rr = (int64_t)blockIdx.x * 4 + wave_id();
   if (rr >= a.R) return;
   const int32_t b0 = a.off[a.E + rr], b1 = a.off[a.E + rr + 1];
   const float* row = a.rel + rr * a.Lr;

@@ -86,18 +86,27 @@ struct RowGeom {
   int half;  // float offset of the imaginary half (complex), 0 otherwise
 };
 
+// Branch-free: every lane loads (a lane past the row end re-reads slot 0, a
+// line the wave fetches anyway) and lanes past the end are zeroed by a select.
+// Only slots s >= NS/2 can be partial (NS is the smallest power of two with
+// 64*NS >= S), so the selects are confined to those.
 template <int NS, int VEC, bool CPLX>
 __device__ __forceinline__ void load_row(const float* __restrict__ base, RowGeom g, int lane,
                                          Row<NS, VEC, CPLX>& r) {
 #pragma unroll
   for (int s = 0; s < NS; ++s) {
     const int slot = lane + 64 * s;
-    if (slot < g.S) {
-      ldv<VEC>(base + slot * VEC, r.a[s]);
-      if constexpr (CPLX) ldv<VEC>(base + g.half + slot * VEC, r.b[s]);
-    } else {
-      zv<VEC>(r.a[s]);
-      if constexpr (CPLX) zv<VEC>(r.b[s]);
+    constexpr bool maybe_partial = true;
+    const bool ok = (s < NS / 2) ? true : (slot < g.S);
+    const int sl = ok ? slot : 0;
+    ldv<VEC>(base + sl * VEC, r.a[s]);
+    if constexpr (CPLX) ldv<VEC>(base + g.half + sl * VEC, r.b[s]);
+    if (maybe_partial && s >= NS / 2) {
+#pragma unroll
+      for (int v = 0; v < VEC; ++v) {
+        r.a[s][v] = ok ? r.a[s][v] : 0.f;
+        if constexpr (CPLX) r.b[s][v] = ok ? r.b[s][v] : 0.f;
+      }
     }
   }
 }
@@ -134,19 +143,39 @@ __device__ __forceinline__ void zero_row(Row<NS, VEC, CPLX>& r) {
   }
 }
 
+// Wave index inside the workgroup as a scalar: threadIdx.x >> 6 is
+// wave-uniform, but only readfirstlane tells the compiler so — and with it
+// every row id and row base address derived from it stays in SGPRs, so the
+// row loads use the scalar-base + 32-bit-lane-offset form.
+__device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
+
 // ------------------------------------------------------------ reductions
+template <int CTRL>
+__device__ __forceinline__ float dppf(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, true));
+}
+__device__ __forceinline__ float readlanef(float v, int l) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+// Full-wave sum, identical bits in every lane, fixed order.  Four DPP steps
+// (lane^1, lane^2, half-row mirror, row mirror) leave each 16-lane row holding
+// its row sum in every lane — each step pairs the same two partial sums on
+// both sides, so the bits agree — then the four row sums are combined as
+// (r0 + r1) + (r2 + r3) from scalar reads.  No LDS traffic.  Must be called
+// with all 64 lanes active.
 __device__ __forceinline__ float wave_sum(float x) {
-  // xor butterfly: every lane ends with the bit-identical total (IEEE add is
-  // commutative and each level pairs the same two partial sums on both sides).
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
-  return x;
+  x = x + dppf<0xB1>(x);   // quad_perm [1,0,3,2]
+  x = x + dppf<0x4E>(x);   // quad_perm [2,3,0,1]
+  x = x + dppf<0x141>(x);  // row_half_mirror
+  x = x + dppf<0x140>(x);  // row_mirror
+  return (readlanef(x, 0) + readlanef(x, 16)) + (readlanef(x, 32) + readlanef(x, 48));
 }
-__device__ __forceinline__ float wave_max(float x) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) x = fmaxf(x, __shfl_xor(x, o, 64));
-  return x;
-}
+
+// Hardware square root / reciprocal (v_sqrt_f32 / v_rcp_f32, ~1 ulp) for the
+// per-element modulus of RotatE; the reference's scalar division (the phase,
+// model.py:209) stays an IEEE division.
+__device__ __forceinline__ float fsqrt(float x) { return __builtin_amdgcn_sqrtf(x); }
+__device__ __forceinline__ float frcp(float x) { return __builtin_amdgcn_rcpf(x); }
 
 __device__ __forceinline__ float sgnf(float x) { return (x > 0.f) ? 1.f : ((x < 0.f) ? -1.f : 0.f); }
 
@@ -210,7 +239,7 @@ struct Elem {
       return HEAD ? (ea * qa + eb * qb) : (qa * ea + qb * eb);  // model.py:192,196
     } else if constexpr (M == ROTATE) {
       const float dr = qa - ea, di = qb - eb;               // model.py:217-223
-      return sqrtf(dr * dr + di * di);                      // stack+norm(dim=0), model.py:225-226
+      return fsqrt(dr * dr + di * di);                      // stack+norm(dim=0), model.py:225-226
     } else {
       const float pe = ea / c.kappa_p;
       const float x = HEAD ? (pe + qa) : (qa - pe);
@@ -240,13 +269,10 @@ struct Elem {
       gqa = ea; gqb = eb; gea = qa; geb = qb;
     } else if constexpr (M == ROTATE) {
       const float dr = qa - ea, di = qb - eb;
-      const float rho = sqrtf(dr * dr + di * di);
-      if (rho > 0.f) {                 // norm backward is masked at 0
-        const float ur = dr / rho, ui = di / rho;
-        gqa = -ur; gqb = -ui; gea = ur; geb = ui;
-      } else {
-        gqa = gqb = gea = geb = 0.f;
-      }
+      const float rho = fsqrt(dr * dr + di * di);
+      const float inv = (rho > 0.f) ? frcp(rho) : 0.f;  // norm backward is masked at 0
+      const float ur = dr * inv, ui = di * inv;
+      gqa = -ur; gqb = -ui; gea = ur; geb = ui;
     } else {
       const float pe = ea / c.kappa_p;
       const float x = HEAD ? (pe + qa) : (qa - pe);
@@ -256,6 +282,48 @@ struct Elem {
       gqa = dx;
       gea = (HEAD ? dx : -dx) / c.kappa_p;
       gqb = geb = 0.f;
+    }
+  }
+
+  // phi for one element, and (ea, eb) overwritten in place with what the
+  // q-gradient needs, so the training row pass evaluates each element once:
+  //   d score / d q = dq_of(ea', eb')  (see dq_of)
+  __device__ static __forceinline__ float phi_dir(float qa, float qb, float& ea, float& eb, const Consts& c) {
+    if constexpr (M == TRANSE) {
+      const float v = HEAD ? (ea + qa) : (qa - ea);
+      ea = sgnf(v);
+      return fabsf(v);
+    } else if constexpr (M == DISTMULT) {
+      return HEAD ? (ea * qa) : (qa * ea);
+    } else if constexpr (M == COMPLEX) {
+      return HEAD ? (ea * qa + eb * qb) : (qa * ea + qb * eb);
+    } else if constexpr (M == ROTATE) {
+      const float dr = qa - ea, di = qb - eb;
+      const float rho = fsqrt(dr * dr + di * di);
+      const float inv = (rho > 0.f) ? frcp(rho) : 0.f;
+      ea = dr * inv;
+      eb = di * inv;
+      return rho;
+    } else {
+      const float pe = ea / c.kappa_p;
+      const float x = HEAD ? (pe + qa) : (qa - pe);
+      float sn, cs;
+      sincosf(x, &sn, &cs);
+      ea = sgnf(sn) * cs;
+      return fabsf(sn);
+    }
+  }
+  // d score / d q from phi_dir's transformed element, scaled by w
+  __device__ static __forceinline__ void dq_of(float ga, float gb, float w, const Consts& c, float& oa, float& ob) {
+    if constexpr (M == TRANSE || M == ROTATE) {
+      oa = -w * ga;
+      ob = -w * gb;
+    } else if constexpr (M == PROTATE) {
+      oa = -(w * c.modulus) * ga;
+      ob = 0.f;
+    } else {
+      oa = w * ga;
+      ob = w * gb;
     }
   }
 

@@ -49,11 +49,14 @@ struct RowArgs {
   const float* g_in;  // ROW_GIVEN: dL/dscore [B, n]
   float* g_out;       // ROW_TRAIN: dL/ds_ij [B, n]
   float* q_out;       // [B, Le]
+  float* dq_out;      // [B, Le]  dL/dq of the negatives (k_row → k_row_epi)
   float* ent_contrib; // [2B, Le]  slot 0 = head row, slot 1 = tail row
   float* rel_contrib; // [B, Lr]
   float* row_stats;   // [B, 4]  logσ(s_pos), neg term, d/dmodulus, s_pos
   int n_lds;          // floats reserved for raw scores in LDS (TRAIN: n)
+  int pipe;           // k_row variant: 1 = next row prefetched (3 waves/SIMD), 0 = 4 waves/SIMD
   int32_t* err;
+  void (*timer_mid)(hipStream_t);  // stage-timer hook between the row-pass launches (or null)
 };
 
 struct EntArgs {
