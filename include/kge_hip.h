@@ -139,6 +139,42 @@ int kge_train_step_grads(const kge_model_desc *m, int32_t mode, const int64_t *p
                          int32_t *err_flag, void *stream);
 
 /*
+ * kge_train_step_grads + the optimizer step, fused — replaces model.py:268-303
+ * (forward, loss, loss.backward() AND optimizer.step()) for a torch.optim.Adam
+ * optimizer (run.py:266-269).  The dense Adam update of every entity /
+ * relation row (zero-gradient rows included, as torch's dense Adam does) is
+ * applied in the gradient passes while each gradient row is in registers, so
+ * gradients are never re-read from HBM.  The parameter pointers must be the
+ * model's own tables (m->entity_embedding etc.; they are updated in place).
+ * Per-tensor step_size = lr / (1 - beta1^t) and bias_correction2_sqrt =
+ * sqrt(1 - beta2^t), computed in double by the caller (torch's formula).
+ * write_grad != 0 also stores the dense gradients into grad_* (as
+ * loss.backward() leaves them in .grad); 0 skips those writes.
+ */
+typedef struct kge_adam_tensor {
+    float *param;
+    float *exp_avg;
+    float *exp_avg_sq;
+    float step_size;
+    float bias_correction2_sqrt;
+} kge_adam_tensor;
+
+typedef struct kge_adam_desc {
+    kge_adam_tensor entity;
+    kge_adam_tensor relation;
+    kge_adam_tensor modulus; /* pRotatE only (param NULL otherwise) */
+    float beta1, beta2, eps;
+    int32_t write_grad;
+} kge_adam_desc;
+
+int kge_train_step(const kge_model_desc *m, int32_t mode, const int64_t *pos, const int64_t *neg,
+                   int64_t batch, int64_t nneg, const float *subsampling_weight, const float *weight_sum,
+                   int32_t uni_weight, int64_t uni_batch, int32_t adversarial, float adversarial_temperature,
+                   float regularization, const kge_adam_desc *adam, float *grad_entity, float *grad_relation,
+                   float *grad_modulus, float *losses_out, void *workspace, size_t workspace_bytes,
+                   int32_t *err_flag, void *stream);
+
+/*
  * Σ subsampling_weight into *out (device scalar) — the denominator of
  * model.py:285-286; exposed so data-parallel ranks can all-reduce it.
  */

@@ -39,6 +39,20 @@ class ModelDesc(C.Structure):
     ]
 
 
+class AdamTensor(C.Structure):
+    """struct kge_adam_tensor."""
+
+    _fields_ = [("param", C.c_void_p), ("exp_avg", C.c_void_p), ("exp_avg_sq", C.c_void_p),
+                ("step_size", C.c_float), ("bias_correction2_sqrt", C.c_float)]
+
+
+class AdamDesc(C.Structure):
+    """struct kge_adam_desc."""
+
+    _fields_ = [("entity", AdamTensor), ("relation", AdamTensor), ("modulus", AdamTensor),
+                ("beta1", C.c_float), ("beta2", C.c_float), ("eps", C.c_float), ("write_grad", C.c_int32)]
+
+
 _P = C.c_void_p
 _I32 = C.c_int32
 _I64 = C.c_int64
@@ -58,6 +72,11 @@ SIGNATURES = {
     "kge_train_step_grads": (
         C.c_int,
         [_DESC, _I32, _P, _P, _I64, _I64, _P, _P, _I32, _I64, _I32, _F, _F, _P, _P, _P, _P, _P, _SZ, _P, _P],
+    ),
+    "kge_train_step": (
+        C.c_int,
+        [_DESC, _I32, _P, _P, _I64, _I64, _P, _P, _I32, _I64, _I32, _F, _F, C.POINTER(AdamDesc), _P, _P, _P, _P, _P,
+         _SZ, _P, _P],
     ),
     "kge_weight_sum": (C.c_int, [_P, _I64, _P, _P]),
     "kge_adam_step": (C.c_int, [_P, _P, _P, _P, _I64, _F, _F, _F, _F, _F, _P]),

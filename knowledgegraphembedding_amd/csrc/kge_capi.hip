@@ -136,8 +136,23 @@ void timer_mark(hipStream_t s) { g_timer.mark(s); }
 // Shared body of backward and train: row pass → CSR → entity pass → relation pass → finalise.
 int run_grad(const kge_model_desc* m, const Geom& geo, int mode, const int64_t* pos, const int64_t* neg,
              int64_t neg_stride, int64_t B, int64_t n, RowArgs ra, GradWs w, float* grad_entity,
-             float* grad_relation, float* grad_modulus, float reg, FinArgs fa, int32_t* err, hipStream_t s) {
+             float* grad_relation, float* grad_modulus, float reg, FinArgs fa, const kge_adam_desc* adam,
+             int32_t* err, hipStream_t s) {
   const ModelOps& op = ops_for(m->model);
+  AdamK ak;
+  ak.b1 = adam ? adam->beta1 : 0.f;
+  ak.b2 = adam ? adam->beta2 : 0.f;
+  ak.eps = adam ? adam->eps : 0.f;
+  auto adam_t = [&](const kge_adam_tensor* t) {
+    AdamT o;
+    o.p = (adam && t && t->param) ? t->param : nullptr;
+    o.m = o.p ? t->exp_avg : nullptr;
+    o.v = o.p ? t->exp_avg_sq : nullptr;
+    o.step_size = o.p ? t->step_size : 0.f;
+    o.bc2s = o.p ? t->bias_correction2_sqrt : 1.f;
+    return o;
+  };
+  const int write_grad = (!adam || adam->write_grad) ? 1 : 0;
   const Consts c = consts_of(m);
   const int Le = m->entity_dim, Lr = m->relation_dim;
   const size_t lds = sizeof(float) * (2 * 64 * (size_t)geo.ns * geo.vec + 2 * (size_t)Le + (size_t)ra.n_lds + 32);
@@ -163,6 +178,9 @@ int run_grad(const kge_model_desc* m, const Geom& geo, int mode, const int64_t* 
   ea.g = (ra.op == ROW_TRAIN) ? w.g : ra.g_in;
   ea.q = w.q; ea.ent_contrib = w.ent_contrib; ea.reg3 = 3.f * reg; ea.reg_partial = w.reg_partial;
   ea.grad_ent = grad_entity;
+  ea.write_grad = write_grad;
+  ea.adam = adam_t(adam ? &adam->entity : nullptr);
+  ea.adamk = ak;
   st = launch_status(op.entity(mode, geo.vec, geo.ns, ea, s));
   if (st) return st;
   if (timed) g_timer.mark(s);
@@ -171,6 +189,9 @@ int run_grad(const kge_model_desc* m, const Geom& geo, int mode, const int64_t* 
   rl.rel = m->relation_embedding; rl.R = m->nrelation; rl.E = m->nentity; rl.B = B; rl.Bn = B * n; rl.Lr = Lr;
   rl.off = w.off; rl.occ = w.occ; rl.rel_contrib = w.rel_contrib; rl.reg3 = 3.f * reg;
   rl.reg_partial = w.reg_partial + m->nentity; rl.grad_rel = grad_relation;
+  rl.write_grad = write_grad;
+  rl.adam = adam_t(adam ? &adam->relation : nullptr);
+  rl.adamk = ak;
   st = launch_status(launch_rel_rows(rl, s));
   if (st) return st;
 
@@ -179,6 +200,8 @@ int run_grad(const kge_model_desc* m, const Geom& geo, int mode, const int64_t* 
   fa.nreg = m->nentity + m->nrelation;
   fa.regularization = reg;
   fa.grad_modulus = grad_modulus;
+  fa.adam = adam_t((adam && m->model == KGE_PROTATE) ? &adam->modulus : nullptr);
+  fa.adamk = ak;
   if (fa.losses || grad_modulus) {
     st = launch_status(launch_finalize(fa, s));
     if (st) return st;
@@ -299,7 +322,7 @@ int kge_score_backward(const kge_model_desc* m, int32_t mode, const int64_t* pos
   fa.losses = nullptr;
   const int kmode = (mode == KGE_HEAD_BATCH) ? HEAD_BATCH : TAIL_BATCH;
   return run_grad(m, geo, kmode, pos, negp, ns, batch, nneg, ra, w, grad_entity, grad_relation,
-                  m->model == KGE_PROTATE ? grad_modulus : nullptr, 0.f, fa, err_flag, as_stream(stream));
+                  m->model == KGE_PROTATE ? grad_modulus : nullptr, 0.f, fa, nullptr, err_flag, as_stream(stream));
 }
 
 size_t kge_train_workspace_bytes(const kge_model_desc* m, int64_t batch, int64_t nneg) {
@@ -308,18 +331,25 @@ size_t kge_train_workspace_bytes(const kge_model_desc* m, int64_t batch, int64_t
   return b;
 }
 
-int kge_train_step_grads(const kge_model_desc* m, int32_t mode, const int64_t* pos, const int64_t* neg,
-                         int64_t batch, int64_t nneg, const float* subsampling_weight, const float* weight_sum,
-                         int32_t uni_weight, int64_t uni_batch, int32_t adversarial,
-                         float adversarial_temperature, float regularization, float* grad_entity,
-                         float* grad_relation, float* grad_modulus, float* losses_out, void* workspace,
-                         size_t workspace_bytes, int32_t* err_flag, void* stream) {
+static int train_impl(const kge_model_desc* m, int32_t mode, const int64_t* pos, const int64_t* neg, int64_t batch,
+                      int64_t nneg, const float* subsampling_weight, const float* weight_sum, int32_t uni_weight,
+                      int64_t uni_batch, int32_t adversarial, float adversarial_temperature, float regularization,
+                      const kge_adam_desc* adam, float* grad_entity, float* grad_relation, float* grad_modulus,
+                      float* losses_out, void* workspace, size_t workspace_bytes, int32_t* err_flag, void* stream) {
   Geom geo;
   int st = check_model(m, &geo);
   if (st) return st;
   if (mode != KGE_HEAD_BATCH && mode != KGE_TAIL_BATCH) return KGE_ERR_MODE;
   if (!pos || !neg || !grad_entity || !grad_relation || !err_flag || !losses_out || batch < 1 || nneg < 1)
     return KGE_ERR_ARG;
+  if (adam) {
+    if (!adam->entity.param || !adam->entity.exp_avg || !adam->entity.exp_avg_sq || !adam->relation.param ||
+        !adam->relation.exp_avg || !adam->relation.exp_avg_sq)
+      return KGE_ERR_ARG;
+    if (adam->entity.param != m->entity_embedding || adam->relation.param != m->relation_embedding)
+      return KGE_ERR_ARG;  // the update is in place on the model's own tables
+    if (m->model == KGE_PROTATE && adam->modulus.param && adam->modulus.param != m->modulus) return KGE_ERR_ARG;
+  }
   if (!uni_weight && !subsampling_weight) return KGE_ERR_ARG;
   if (m->model == KGE_PROTATE && !grad_modulus) return KGE_ERR_ARG;
   size_t need = 0;
@@ -352,7 +382,29 @@ int kge_train_step_grads(const kge_model_desc* m, int32_t mode, const int64_t* p
   fa.uni_n = (float)ub;
   fa.losses = losses_out;
   return run_grad(m, geo, mode, pos, neg, nneg, batch, nneg, ra, w, grad_entity, grad_relation,
-                  m->model == KGE_PROTATE ? grad_modulus : nullptr, regularization, fa, err_flag, s);
+                  m->model == KGE_PROTATE ? grad_modulus : nullptr, regularization, fa, adam, err_flag, s);
+}
+
+int kge_train_step_grads(const kge_model_desc* m, int32_t mode, const int64_t* pos, const int64_t* neg,
+                         int64_t batch, int64_t nneg, const float* subsampling_weight, const float* weight_sum,
+                         int32_t uni_weight, int64_t uni_batch, int32_t adversarial,
+                         float adversarial_temperature, float regularization, float* grad_entity,
+                         float* grad_relation, float* grad_modulus, float* losses_out, void* workspace,
+                         size_t workspace_bytes, int32_t* err_flag, void* stream) {
+  return train_impl(m, mode, pos, neg, batch, nneg, subsampling_weight, weight_sum, uni_weight, uni_batch, adversarial,
+                    adversarial_temperature, regularization, nullptr, grad_entity, grad_relation, grad_modulus,
+                    losses_out, workspace, workspace_bytes, err_flag, stream);
+}
+
+int kge_train_step(const kge_model_desc* m, int32_t mode, const int64_t* pos, const int64_t* neg, int64_t batch,
+                   int64_t nneg, const float* subsampling_weight, const float* weight_sum, int32_t uni_weight,
+                   int64_t uni_batch, int32_t adversarial, float adversarial_temperature, float regularization,
+                   const kge_adam_desc* adam, float* grad_entity, float* grad_relation, float* grad_modulus,
+                   float* losses_out, void* workspace, size_t workspace_bytes, int32_t* err_flag, void* stream) {
+  if (!adam) return KGE_ERR_ARG;
+  return train_impl(m, mode, pos, neg, batch, nneg, subsampling_weight, weight_sum, uni_weight, uni_batch, adversarial,
+                    adversarial_temperature, regularization, adam, grad_entity, grad_relation, grad_modulus,
+                    losses_out, workspace, workspace_bytes, err_flag, stream);
 }
 
 int kge_weight_sum(const float* w, int64_t n, float* out, void* stream) {

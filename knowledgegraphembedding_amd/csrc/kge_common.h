@@ -27,6 +27,9 @@ struct RelArgs {
   float reg3;
   float* reg_partial;        // [R]
   float* grad_rel;
+  int write_grad;            // store grad_rel (always, unless the optimizer is fused and asks not to)
+  AdamT adam;                // fused optimizer step (adam.p == null: none)
+  AdamK adamk;
 };
 
 struct FinArgs {
@@ -41,6 +44,8 @@ struct FinArgs {
   float regularization;
   float* losses;             // [4]
   float* grad_modulus;       // nullable
+  AdamT adam;                // fused optimizer step of the pRotatE modulus (adam.p == null: none)
+  AdamK adamk;
 };
 
 int launch_csr(const CsrArgs& a, hipStream_t s);

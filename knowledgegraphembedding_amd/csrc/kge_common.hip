@@ -89,37 +89,62 @@ __global__ __launch_bounds__(256) void k_csr_rank(CsrArgs a) {
 
 // -------------------------------------------------- relation gradient rows
 // One wave per relation row: Σ of the rows' relation contributions in id
-// order (+ 3λ r|r|), written densely.
-__global__ __launch_bounds__(256) void k_rel_rows(RelArgs a) {
-  const int lane = threadIdx.x & 63;
-  const int64_t rr = (int64_t)blockIdx.x * 4 + wave_id();
-  if (rr >= a.R) return;
+// order (+ 3λ r|r|), written densely; with a fused optimizer the Adam update
+// of the row is applied while the gradient is in registers.  Lanes own float4
+// chunks c = lane + 64u of the row (scalar tail when Lr % 4 != 0).
+template <int U>
+__device__ __forceinline__ void rel_row_chunks(const RelArgs& a, int64_t rr, int lane) {
   const int32_t b0 = a.off[a.E + rr], b1 = a.off[a.E + rr + 1];
   const float* row = a.rel + rr * a.Lr;
-  float* out = a.grad_rel + rr * a.Lr;
+  const bool v4 = (a.Lr % 4) == 0;
+  const int nchunk = v4 ? a.Lr / 4 : a.Lr;  // float4 chunks, or single floats
   float part = 0.f;
-  for (int k0 = 0; k0 < a.Lr; k0 += 64 * 4) {
-    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int c0 = 0; c0 < nchunk; c0 += 64 * U) {
+    float acc[U][4];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) acc[u][e] = 0.f;
     for (int32_t p = b0; p < b1; ++p) {
       const int64_t i = a.occ[p] - a.Bn - 2 * a.B;
       const float* src = a.rel_contrib + i * a.Lr;
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int k = k0 + u * 64 + lane;
-        if (k < a.Lr) acc[u] += src[k];
+      for (int u = 0; u < U; ++u) {
+        const int c = c0 + u * 64 + lane;
+        if (c < nchunk) {
+          if (v4) {
+            const float4 x = reinterpret_cast<const float4*>(src)[c];
+            acc[u][0] += x.x; acc[u][1] += x.y; acc[u][2] += x.z; acc[u][3] += x.w;
+          } else {
+            acc[u][0] += src[c];
+          }
+        }
       }
     }
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int k = k0 + u * 64 + lane;
-      if (k < a.Lr) {
-        float v = acc[u];
+    for (int u = 0; u < U; ++u) {
+      const int c = c0 + u * 64 + lane;
+      if (c >= nchunk) continue;
+      const int nel = v4 ? 4 : 1;
+      const int k0 = v4 ? 4 * c : c;
+      float x[4] = {0.f, 0.f, 0.f, 0.f};
+      for (int e = 0; e < nel; ++e) x[e] = row[k0 + e];
+      for (int e = 0; e < nel; ++e) {
         if (a.reg3 != 0.f) {
-          const float x = row[k];
-          v += a.reg3 * (x * fabsf(x));
-          part += fabsf(x) * x * x;
+          acc[u][e] += a.reg3 * (x[e] * fabsf(x[e]));
+          part += fabsf(x[e]) * x[e] * x[e];
         }
-        out[k] = v;
+        if (a.write_grad) a.grad_rel[rr * a.Lr + k0 + e] = acc[u][e];
+      }
+      if (a.adam.p) {
+        float* P = a.adam.p + rr * a.Lr + k0;
+        float* Mm = a.adam.m + rr * a.Lr + k0;
+        float* Vv = a.adam.v + rr * a.Lr + k0;
+        for (int e = 0; e < nel; ++e) {
+          float pv = x[e], mv = Mm[e], vv = Vv[e];
+          adam_elem(pv, acc[u][e], mv, vv, a.adamk, a.adam.step_size, a.adam.bc2s);
+          P[e] = pv; Mm[e] = mv; Vv[e] = vv;
+        }
       }
     }
   }
@@ -127,6 +152,13 @@ __global__ __launch_bounds__(256) void k_rel_rows(RelArgs a) {
     part = wave_sum(part);
     if (lane == 0) a.reg_partial[rr] = part;
   }
+}
+
+__global__ __launch_bounds__(256) void k_rel_rows(RelArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int64_t rr = (int64_t)blockIdx.x * 4 + wave_id();
+  if (rr >= a.R) return;
+  rel_row_chunks<4>(a, rr, lane);
 }
 
 // ------------------------------------------------------------ finalise
@@ -191,6 +223,11 @@ __global__ __launch_bounds__(1024) void k_finalize(FinArgs a) {
       a.losses[3] = reg;
     }
     if (a.grad_modulus) a.grad_modulus[0] = tot[5];
+    if (a.adam.p) {  // pRotatE modulus, fused optimizer step
+      float pv = a.adam.p[0], mv = a.adam.m[0], vv = a.adam.v[0];
+      adam_elem(pv, tot[5], mv, vv, a.adamk, a.adam.step_size, a.adam.bc2s);
+      a.adam.p[0] = pv; a.adam.m[0] = mv; a.adam.v[0] = vv;
+    }
   }
 }
 
@@ -209,39 +246,28 @@ __global__ __launch_bounds__(1024) void k_weight_sum(const float* __restrict__ w
 }
 
 // ------------------------------------------------------------------ Adam
-// torch.optim.Adam single-tensor math (torch/optim/adam.py, non-capturable):
-//   m.lerp_(g, 1-b1); v.mul_(b2).addcmul_(g, g, 1-b2);
-//   denom = v.sqrt() / bc2_sqrt + eps; p.addcdiv_(m, denom, -step_size)
-__device__ __forceinline__ void adam_elem(float& p, float g, float& m, float& v, float b1, float b2, float eps,
-                                          float step_size, float bc2s) {
-  const float w = 1.f - b1;  // lerp weight < 0.5 → self + w * (end - self)
-  m = m + w * (g - m);
-  v = v * b2 + (1.f - b2) * (g * g);
-  const float denom = sqrtf(v) / bc2s + eps;
-  p = p + (-step_size) * (m / denom);
-}
-
+// Standalone dense Adam over one tensor (KGEAdam.step / kge_adam_step).
 __global__ __launch_bounds__(256) void k_adam(float* __restrict__ p, const float* __restrict__ g,
-                                              float* __restrict__ m, float* __restrict__ v, int64_t n, float b1,
-                                              float b2, float eps, float step_size, float bc2s) {
+                                              float* __restrict__ m, float* __restrict__ v, int64_t n, AdamK k,
+                                              float step_size, float bc2s) {
   const int64_t n4 = n / 4;
-  for (int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x; k < n4; k += (int64_t)gridDim.x * 256) {
-    float4 P = reinterpret_cast<float4*>(p)[k];
-    const float4 G = reinterpret_cast<const float4*>(g)[k];
-    float4 Mv = reinterpret_cast<float4*>(m)[k];
-    float4 Vv = reinterpret_cast<float4*>(v)[k];
-    adam_elem(P.x, G.x, Mv.x, Vv.x, b1, b2, eps, step_size, bc2s);
-    adam_elem(P.y, G.y, Mv.y, Vv.y, b1, b2, eps, step_size, bc2s);
-    adam_elem(P.z, G.z, Mv.z, Vv.z, b1, b2, eps, step_size, bc2s);
-    adam_elem(P.w, G.w, Mv.w, Vv.w, b1, b2, eps, step_size, bc2s);
-    reinterpret_cast<float4*>(p)[k] = P;
-    reinterpret_cast<float4*>(m)[k] = Mv;
-    reinterpret_cast<float4*>(v)[k] = Vv;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
+    float4 P = reinterpret_cast<float4*>(p)[i];
+    const float4 G = reinterpret_cast<const float4*>(g)[i];
+    float4 Mv = reinterpret_cast<float4*>(m)[i];
+    float4 Vv = reinterpret_cast<float4*>(v)[i];
+    adam_elem(P.x, G.x, Mv.x, Vv.x, k, step_size, bc2s);
+    adam_elem(P.y, G.y, Mv.y, Vv.y, k, step_size, bc2s);
+    adam_elem(P.z, G.z, Mv.z, Vv.z, k, step_size, bc2s);
+    adam_elem(P.w, G.w, Mv.w, Vv.w, k, step_size, bc2s);
+    reinterpret_cast<float4*>(p)[i] = P;
+    reinterpret_cast<float4*>(m)[i] = Mv;
+    reinterpret_cast<float4*>(v)[i] = Vv;
   }
-  for (int64_t k = n4 * 4 + (int64_t)blockIdx.x * 256 + threadIdx.x; k < n; k += (int64_t)gridDim.x * 256) {
-    float P = p[k], Mv = m[k], Vv = v[k];
-    adam_elem(P, g[k], Mv, Vv, b1, b2, eps, step_size, bc2s);
-    p[k] = P; m[k] = Mv; v[k] = Vv;
+  for (int64_t i = n4 * 4 + (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    float P = p[i], Mv = m[i], Vv = v[i];
+    adam_elem(P, g[i], Mv, Vv, k, step_size, bc2s);
+    p[i] = P; m[i] = Mv; v[i] = Vv;
   }
 }
 
@@ -281,8 +307,9 @@ int launch_weight_sum(const float* w, int64_t n, float* out, hipStream_t s) {
 
 int launch_adam(float* p, const float* g, float* m, float* v, int64_t n, float b1, float b2, float eps,
                 float step_size, float bc2s, hipStream_t s) {
-  hipLaunchKernelGGL(k_adam, dim3(grid_for((n + 3) / 4, 8192)), dim3(256), 0, s, p, g, m, v, n, b1, b2, eps,
-                     step_size, bc2s);
+  AdamK k;
+  k.b1 = b1; k.b2 = b2; k.eps = eps;
+  hipLaunchKernelGGL(k_adam, dim3(grid_for((n + 3) / 4, 8192)), dim3(256), 0, s, p, g, m, v, n, k, step_size, bc2s);
   return (int)hipGetLastError();
 }
 

@@ -185,6 +185,28 @@ __device__ __forceinline__ float log_sigmoid(float x) {
 }
 __device__ __forceinline__ float sigmoidf(float x) { return 1.f / (1.f + expf(-x)); }
 
+// torch.optim.Adam single-tensor update of one element (torch/optim/adam.py,
+// non-capturable branch; run.py:266-269 builds it with the defaults):
+//   m.lerp_(g, 1-b1); v.mul_(b2).addcmul_(g, g, 1-b2);
+//   denom = v.sqrt() / bias_correction2_sqrt + eps; p.addcdiv_(m, denom, -step_size)
+struct AdamT {
+  float* p;
+  float* m;
+  float* v;
+  float step_size, bc2s;
+};
+struct AdamK {
+  float b1, b2, eps;
+};
+__device__ __forceinline__ void adam_elem(float& p, float g, float& m, float& v, const AdamK& k, float step_size,
+                                          float bc2s) {
+  const float w = 1.f - k.b1;  // lerp weight < 0.5 → self + w * (end - self)
+  m = m + w * (g - m);
+  v = v * k.b2 + (1.f - k.b2) * (g * g);
+  const float denom = sqrtf(v) / bc2s + k.eps;
+  p = p + (-step_size) * (m / denom);
+}
+
 // ------------------------------------------------------------ model math
 // q construction for the element (a, b) of one slot.
 //   TAIL/SINGLE: inputs (x = head, r); HEAD: inputs (r, x = tail)

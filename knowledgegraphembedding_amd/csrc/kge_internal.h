@@ -76,6 +76,9 @@ struct EntArgs {
   float reg3;           // 3 * regularization (0 = off)
   float* reg_partial;   // [E] Σ|x|^3 per row (when reg3 != 0)
   float* grad_ent;
+  int write_grad;       // store grad_ent (unless the fused optimizer asks not to)
+  AdamT adam;           // fused optimizer step (adam.p == null: none)
+  AdamK adamk;
 };
 
 struct RankArgs {

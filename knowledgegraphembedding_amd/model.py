@@ -89,6 +89,9 @@ class KGEModel(nn.Module):
 
         self._scalars = None
         self._grad_bufs = None
+        # leave the dense gradients in .grad after a fused train_step, as
+        # loss.backward() does in the reference; False skips those writes
+        self.keep_grads = True
 
     # ------------------------------------------------------------------ helpers
     def _host_scalars(self):
@@ -191,20 +194,26 @@ class KGEModel(nn.Module):
         return bufs
 
     def compute_train_grads(self, positive_sample, negative_sample, subsampling_weight, mode, args,
-                            weight_sum=None, uni_batch=0):
+                            weight_sum=None, uni_batch=0, optimizer=None):
         """Fused forward + self-adversarial loss + backward (model.py:268-301).
         Writes dense .grad tensors; returns the device [4] loss vector
-        (positive_sample_loss, negative_sample_loss, loss, regularization)."""
+        (positive_sample_loss, negative_sample_loss, loss, regularization).
+        With a KGEAdam `optimizer` the Adam update is applied inside the same
+        gradient passes (the optimizer's next step() then skips these tables)."""
         dev = ops._require_device(self.entity_embedding)
         g, rng = self._host_scalars()
         ge, gr, gm, losses = self._grad_buffers()
+        adam = None
+        if optimizer is not None and hasattr(optimizer, 'prepare_fused'):
+            adam = optimizer.prepare_fused(self.entity_embedding, self.relation_embedding, self._modulus(),
+                                           write_grad=self.keep_grads)
         ops.train_step_grads(
             self.desc(), mode, positive_sample, negative_sample, subsampling_weight, dev,
             adversarial=bool(args.negative_adversarial_sampling),
             temperature=float(getattr(args, 'adversarial_temperature', 1.0)),
             uni_weight=bool(args.uni_weight), regularization=float(args.regularization),
             grad_entity=ge, grad_relation=gr, grad_modulus=gm, losses=losses,
-            weight_sum_dev=weight_sum, uni_batch=uni_batch)
+            weight_sum_dev=weight_sum, uni_batch=uni_batch, adam=adam)
         if self.entity_embedding.requires_grad:
             self.entity_embedding.grad = ge
         if self.relation_embedding.requires_grad:
@@ -234,7 +243,10 @@ class KGEModel(nn.Module):
             from .distributed import dp_train_grads
             losses = dp_train_grads(model, positive_sample, negative_sample, subsampling_weight, mode, args)
         else:
-            losses = model.compute_train_grads(positive_sample, negative_sample, subsampling_weight, mode, args)
+            # a KGEAdam optimizer is stepped inside the gradient passes; any
+            # other optimizer sees ordinary dense .grad tensors
+            losses = model.compute_train_grads(positive_sample, negative_sample, subsampling_weight, mode, args,
+                                               optimizer=optimizer)
 
         optimizer.step()
 

@@ -172,8 +172,9 @@ def train_step_grads(desc: _lib.ModelDesc, mode: str, pos: torch.Tensor, neg: to
                      dev, *, adversarial: bool, temperature: float, uni_weight: bool, regularization: float,
                      grad_entity: torch.Tensor, grad_relation: torch.Tensor, grad_modulus: Optional[torch.Tensor],
                      losses: torch.Tensor, weight_sum_dev: Optional[torch.Tensor] = None,
-                     uni_batch: int = 0) -> None:
-    """Fused scoring + loss + backward into the given dense grad buffers (model.py:252-301)."""
+                     uni_batch: int = 0, adam: Optional[_lib.AdamDesc] = None) -> None:
+    """Fused scoring + loss + backward into the given dense grad buffers (model.py:252-301);
+    with `adam`, also the optimizer step, fused into the gradient passes (model.py:303)."""
     if mode not in ("head-batch", "tail-batch"):
         raise ValueError("Training batch mode %s not supported" % mode)
     pos = _idx(pos, dev)
@@ -184,14 +185,14 @@ def train_step_grads(desc: _lib.ModelDesc, mode: str, pos: torch.Tensor, neg: to
     need = lib.kge_train_workspace_bytes(desc, B, n)
     st = state(dev)
     ws = st.workspace(need)
-    _lib.check(
-        lib.kge_train_step_grads(
-            desc, _lib.MODE_IDS[mode], pos.data_ptr(), neg.data_ptr(), B, n, w.data_ptr(), _ptr(weight_sum_dev),
-            int(bool(uni_weight)), int(uni_batch), int(bool(adversarial)), float(temperature), float(regularization),
-            grad_entity.data_ptr(), grad_relation.data_ptr(), _ptr(grad_modulus), losses.data_ptr(), ws.data_ptr(),
-            ws.numel(), st.err.data_ptr(), _stream(dev)),
-        "kge_train_step_grads",
-    )
+    common = (desc, _lib.MODE_IDS[mode], pos.data_ptr(), neg.data_ptr(), B, n, w.data_ptr(), _ptr(weight_sum_dev),
+              int(bool(uni_weight)), int(uni_batch), int(bool(adversarial)), float(temperature), float(regularization))
+    tail = (grad_entity.data_ptr(), grad_relation.data_ptr(), _ptr(grad_modulus), losses.data_ptr(), ws.data_ptr(),
+            ws.numel(), st.err.data_ptr(), _stream(dev))
+    if adam is None:
+        _lib.check(lib.kge_train_step_grads(*common, *tail), "kge_train_step_grads")
+    else:
+        _lib.check(lib.kge_train_step(*common, adam, *tail), "kge_train_step")
 
 
 def adam_step(param: torch.Tensor, grad: torch.Tensor, exp_avg: torch.Tensor, exp_avg_sq: torch.Tensor, *,

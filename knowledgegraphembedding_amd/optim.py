@@ -9,6 +9,8 @@ SURVEY §7 hard part vii) runs in kge_adam_step.
 """
 from __future__ import annotations
 
+import math
+
 import torch
 
 from . import ops
@@ -23,24 +25,67 @@ class KGEAdam(torch.optim.Optimizer):
                         foreach=None, capturable=False, differentiable=False, fused=None)
         super().__init__(params, defaults)
 
+        self._fused_done = set()
+
+    def _group_of(self, p):
+        for g in self.param_groups:
+            for q in g['params']:
+                if q is p:
+                    return g
+        return None
+
+    def _advance(self, p, group):
+        state = self.state[p]
+        if len(state) == 0:
+            state['step'] = torch.tensor(0.0)
+            state['exp_avg'] = torch.zeros_like(p, memory_format=torch.preserve_format)
+            state['exp_avg_sq'] = torch.zeros_like(p, memory_format=torch.preserve_format)
+        state['step'] += 1
+        return state, int(state['step'].item())
+
+    def prepare_fused(self, entity, relation, modulus=None, write_grad=True):
+        """Adam descriptor for kge_train_step, which applies this optimizer's
+        update to the tables inside the gradient passes.  Advances the step
+        counters now and marks the tensors so the following step() skips them.
+        Returns None (use the unfused path) if the configuration does not fit."""
+        from . import _lib
+        tensors = [entity, relation] + ([modulus] if modulus is not None else [])
+        groups = [self._group_of(p) for p in tensors]
+        if any(g is None for g in groups) or any(not p.requires_grad for p in tensors):
+            return None
+        if len({(g['betas'], g['eps']) for g in groups}) != 1:
+            return None
+        if any(not p.is_contiguous() for p in tensors):
+            return None
+        desc = _lib.AdamDesc()
+        beta1, beta2 = groups[0]['betas']
+        desc.beta1, desc.beta2, desc.eps = beta1, beta2, groups[0]['eps']
+        desc.write_grad = 1 if write_grad else 0
+        for p, g, field in zip(tensors, groups, ('entity', 'relation', 'modulus')):
+            state, step = self._advance(p, g)
+            t = getattr(desc, field)
+            t.param = p.data_ptr()
+            t.exp_avg = state['exp_avg'].data_ptr()
+            t.exp_avg_sq = state['exp_avg_sq'].data_ptr()
+            t.step_size = g['lr'] / (1 - beta1 ** step)
+            t.bias_correction2_sqrt = math.sqrt(1 - beta2 ** step)
+            self._fused_done.add(id(p))
+        return desc
+
     @torch.no_grad()
     def step(self, closure=None):
         loss = None
         if closure is not None:
             with torch.enable_grad():
                 loss = closure()
+        done, self._fused_done = self._fused_done, set()
         for group in self.param_groups:
             beta1, beta2 = group['betas']
             for p in group['params']:
-                if p.grad is None:
+                if p.grad is None or id(p) in done:
                     continue
-                state = self.state[p]
-                if len(state) == 0:
-                    state['step'] = torch.tensor(0.0)
-                    state['exp_avg'] = torch.zeros_like(p, memory_format=torch.preserve_format)
-                    state['exp_avg_sq'] = torch.zeros_like(p, memory_format=torch.preserve_format)
-                state['step'] += 1
+                state, step = self._advance(p, group)
                 grad = p.grad if p.grad.is_contiguous() else p.grad.contiguous()
-                ops.adam_step(p.data, grad, state['exp_avg'], state['exp_avg_sq'], step=int(state['step'].item()),
+                ops.adam_step(p.data, grad, state['exp_avg'], state['exp_avg_sq'], step=step,
                               lr=group['lr'], beta1=beta1, beta2=beta2, eps=group['eps'])
         return loss

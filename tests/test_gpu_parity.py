@@ -165,6 +165,53 @@ def test_train_grads_deterministic():
         assert torch.equal(a, b)
 
 
+def test_fused_adam_train_step_vs_golden(g_train, golden_info):
+    """KGEModel.train_step with KGEAdam (Adam fused into the gradient passes)
+    against the reference's params after two steps."""
+    for ci in range(0, len(golden_info["train"]["cases"]), 3):
+        m, args, batch, case, ti = _train_case(g_train, golden_info, ci)
+        opt = KGEAdam([p for p in m.parameters() if p.requires_grad], lr=ti["lr"])
+        log = KGEModel.train_step(m, opt, iter([batch]), args)
+        KGEModel.train_step(m, opt, iter([batch]), args)
+        ref = g_train[f"{ci}/log"]
+        got = np.array([log["positive_sample_loss"], log["negative_sample_loss"], log["loss"],
+                        log.get("regularization", 0.0)])
+        assert np.all(np.abs(got - ref) <= score_tol(ref)), f"{case} log"
+        p2 = m.entity_embedding.detach().cpu().numpy()
+        assert np.abs(p2 - g_train[f"{ci}/param2_entity"]).max() <= 2e-4 * 0.01 * 2 + 1e-6, f"{case} entity"
+        r2 = m.relation_embedding.detach().cpu().numpy()
+        assert np.abs(r2 - g_train[f"{ci}/param2_relation"]).max() <= 2e-4 * 0.01 * 2 + 1e-6, f"{case} relation"
+        if case["model"] == "pRotatE":
+            mo = m.modulus.detach().cpu().numpy()
+            assert np.abs(mo - g_train[f"{ci}/param2_modulus"]).max() <= 1e-5, f"{case} modulus"
+        assert opt.state[m.entity_embedding]["step"].item() == 2
+
+
+@pytest.mark.parametrize("name", NAMES)
+def test_fused_adam_bitwise_equals_unfused(name):
+    """The fused optimizer step applies the same per-element Adam to the same
+    deterministic gradients as KGEAdam.step(): parameters, moments and grads
+    must agree bit for bit over several steps."""
+    E, R, d, B, n = 700, 9, 64, 32, 48
+    runs = []
+    for fused in (True, False):
+        m, *_ = build_model(name, E, R, d, 12.0, 31)
+        opt = KGEAdam([p for p in m.parameters() if p.requires_grad], lr=3e-3)
+        args = Namespace(negative_adversarial_sampling=True, adversarial_temperature=0.5, uni_weight=False,
+                         regularization=1e-4 if name in ("DistMult", "ComplEx") else 0.0)
+        for step in range(3):
+            pos, neg, w = synth.kge_batch(40 + step, B, n, E, R)
+            mode = "tail-batch" if step % 2 == 0 else "head-batch"
+            m.compute_train_grads(torch.from_numpy(pos).to(DEV), torch.from_numpy(neg).to(DEV),
+                                  torch.from_numpy(w).to(DEV), mode, args, optimizer=opt if fused else None)
+            opt.step()
+        st = opt.state[m.entity_embedding]
+        runs.append([t.detach().cpu().clone() for t in (m.entity_embedding, m.relation_embedding,
+                                                        st["exp_avg"], st["exp_avg_sq"], m.entity_embedding.grad)])
+    for a, b in zip(*runs):
+        assert torch.equal(a, b)
+
+
 # ------------------------------------------------------------ forward autograd
 @pytest.mark.parametrize("name", NAMES)
 @pytest.mark.parametrize("mode", ["single", "head-batch", "tail-batch"])
