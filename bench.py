@@ -192,8 +192,8 @@ def main():
                    "negatives": NNEG, "adversarial_temperature": TEMP, "gamma": GAMMA,
                    "parallelism": f"dp{world}"},
         "stage_ms": {"build_q": float(stage[0]) / calls, "row_pass": row_ms, "row_epilogue": float(stage[2]) / calls,
-                     "csr": float(stage[3]) / calls, "entity_pass": float(stage[4]) / calls,
-                     "relation_pass_finalize": float(stage[5]) / calls,
+                     "csr_join": float(stage[3]) / calls, "entity_pass": float(stage[4]) / calls,
+                     "relation_join_finalize": float(stage[5]) / calls,
                      "other_incl_adam_ms": dt / a.steps * 1e3 - float(stage[:6].sum()) / calls},
         "roofline": {"bound": "hbm", "kernel": "k_row (fused negative scoring + self-adversarial loss)",
                      "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,

@@ -212,9 +212,11 @@ int kge_rank_filtered(const kge_model_desc *m, int32_t mode, const int64_t *quer
 /*
  * Live stage timing for benchmarks (no reference counterpart): when enabled,
  * kge_train_step_grads records a hipEvent on its stream before and after each
- * stage — 0 q build, 1 fused negative scoring + self-adversarial loss (the
- * gather loop), 2 positive score + chain rule, 3 occurrence CSR, 4
- * entity-major gradient pass, 5 relation pass + loss finalisation.
+ * stage of the caller's stream — 0 q build, 1 fused negative scoring +
+ * self-adversarial loss (the gather loop), 2 positive score + chain rule,
+ * 3 wait for the occurrence CSR (built on an internal side stream in parallel
+ * with stages 0-2), 4 entity-major gradient pass (+ fused Adam), 5 wait for the
+ * relation pass (side stream, parallel with 4) + loss finalisation.
  *   command 1: enable and reset; 0: disable and reset;
  *   command 2: synchronise the recorded events and write the summed
  *              milliseconds per stage to stage_ms_out[0..5] and the number of

@@ -133,7 +133,31 @@ struct StageTimer {
 StageTimer g_timer;
 void timer_mark(hipStream_t s) { g_timer.mark(s); }
 
-// Shared body of backward and train: row pass → CSR → entity pass → relation pass → finalise.
+// ---- side stream: the index-only work (occurrence CSR) and the relation
+// pass run beside the gather kernels of the caller's stream.  Fork/join via
+// events (a pattern stream capture records as graph edges); the caller's
+// stream never runs ahead of anything the side stream still reads or writes.
+struct Side {
+  hipStream_t s = nullptr;
+  hipEvent_t fork = nullptr, csr_done = nullptr, epi_done = nullptr, rel_done = nullptr;
+};
+Side* side_for_device() {
+  static Side sides[64];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  Side& sd = sides[dev];
+  if (!sd.s) {
+    if (hipStreamCreateWithFlags(&sd.s, hipStreamNonBlocking) != hipSuccess) return nullptr;
+    hipEventCreateWithFlags(&sd.fork, hipEventDisableTiming);
+    hipEventCreateWithFlags(&sd.csr_done, hipEventDisableTiming);
+    hipEventCreateWithFlags(&sd.epi_done, hipEventDisableTiming);
+    hipEventCreateWithFlags(&sd.rel_done, hipEventDisableTiming);
+  }
+  return &sd;
+}
+
+// Shared body of backward and train.  Caller's stream: q build → gather loop →
+// epilogue → entity pass → finalise; side stream: CSR ∥ row pass, relation pass ∥ entity pass.
 int run_grad(const kge_model_desc* m, const Geom& geo, int mode, const int64_t* pos, const int64_t* neg,
              int64_t neg_stride, int64_t B, int64_t n, RowArgs ra, GradWs w, float* grad_entity,
              float* grad_relation, float* grad_modulus, float reg, FinArgs fa, const kge_adam_desc* adam,
@@ -159,17 +183,47 @@ int run_grad(const kge_model_desc* m, const Geom& geo, int mode, const int64_t* 
   if (lds > 64 * 1024) return KGE_ERR_DIM;
   const bool timed = g_timer.on && ra.op == ROW_TRAIN;
   ra.timer_mid = timed ? &timer_mark : nullptr;
-  if (timed) g_timer.mark(s);
-  int st = launch_status(op.row(mode, geo.vec, geo.ns, ra, lds, s));
-  if (st) return st;
-  if (timed) g_timer.mark(s);
+  Side* sd = side_for_device();
+  hipStream_t ss = sd ? sd->s : s;
+  int st;
 
+  // fork: the occurrence CSR needs only the batch indices
   CsrArgs ca;
   ca.pos = pos; ca.neg = neg; ca.neg_stride = neg_stride;
   ca.B = B; ca.n = n; ca.Bn = B * n; ca.E = m->nentity; ca.R = m->nrelation;
   ca.keys = w.keys; ca.cnt = w.cnt; ca.off = w.off; ca.tmp = w.tmp; ca.occ = w.occ; ca.err = err;
-  st = launch_status(launch_csr(ca, s));
+  if (sd) {
+    hipEventRecord(sd->fork, s);
+    hipStreamWaitEvent(ss, sd->fork, 0);
+  }
+  st = launch_status(launch_csr(ca, ss));
   if (st) return st;
+  if (sd) hipEventRecord(sd->csr_done, ss);
+
+  // row pass on the caller's stream: q build | gather loop | epilogue
+  if (timed) g_timer.mark(s);
+  st = launch_status(op.row(mode, geo.vec, geo.ns, ra, lds, s));
+  if (st) return st;
+  if (timed) g_timer.mark(s);
+
+  // relation pass on the side stream once the epilogue's contributions exist
+  RelArgs rl;
+  rl.rel = m->relation_embedding; rl.R = m->nrelation; rl.E = m->nentity; rl.B = B; rl.Bn = B * n; rl.Lr = Lr;
+  rl.off = w.off; rl.occ = w.occ; rl.rel_contrib = w.rel_contrib; rl.reg3 = 3.f * reg;
+  rl.reg_partial = w.reg_partial + m->nentity; rl.grad_rel = grad_relation;
+  rl.write_grad = write_grad;
+  rl.adam = adam_t(adam ? &adam->relation : nullptr);
+  rl.adamk = ak;
+  if (sd) {
+    hipEventRecord(sd->epi_done, s);
+    hipStreamWaitEvent(ss, sd->epi_done, 0);
+  }
+  st = launch_status(launch_rel_rows(rl, ss));
+  if (st) return st;
+  if (sd) {
+    hipEventRecord(sd->rel_done, ss);
+    hipStreamWaitEvent(s, sd->csr_done, 0);  // join 1: the entity pass reads the CSR
+  }
   if (timed) g_timer.mark(s);
 
   EntArgs ea;
@@ -185,16 +239,7 @@ int run_grad(const kge_model_desc* m, const Geom& geo, int mode, const int64_t* 
   if (st) return st;
   if (timed) g_timer.mark(s);
 
-  RelArgs rl;
-  rl.rel = m->relation_embedding; rl.R = m->nrelation; rl.E = m->nentity; rl.B = B; rl.Bn = B * n; rl.Lr = Lr;
-  rl.off = w.off; rl.occ = w.occ; rl.rel_contrib = w.rel_contrib; rl.reg3 = 3.f * reg;
-  rl.reg_partial = w.reg_partial + m->nentity; rl.grad_rel = grad_relation;
-  rl.write_grad = write_grad;
-  rl.adam = adam_t(adam ? &adam->relation : nullptr);
-  rl.adamk = ak;
-  st = launch_status(launch_rel_rows(rl, s));
-  if (st) return st;
-
+  if (sd) hipStreamWaitEvent(s, sd->rel_done, 0);  // join 2: everything the side stream wrote
   fa.row_stats = w.row_stats;
   fa.reg_partial = (reg != 0.f) ? w.reg_partial : nullptr;
   fa.nreg = m->nentity + m->nrelation;
