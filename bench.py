@@ -134,6 +134,8 @@ def main():
     erange = model.embedding_range.item()
     cpu_state = (model.entity_embedding.detach().clone(), model.relation_embedding.detach().clone(), erange)
     model = model.to(dev)
+    model.fuse_optimizer = os.environ.get("KGE_FUSED_ADAM", "1") == "1"
+    model.keep_grads = os.environ.get("KGE_KEEP_GRADS", "1") == "1"
     args = Namespace(cuda=True, negative_adversarial_sampling=True, adversarial_temperature=TEMP, uni_weight=False,
                      regularization=0.0, dp_group=group)
     opt = KGEAdam([p for p in model.parameters() if p.requires_grad], lr=1e-4)
@@ -187,6 +189,8 @@ def main():
         "vs_baseline": None,
         "dtype": "fp32",
         "data": "synthetic (uniform ids, U(-range,range) tables), batches pre-staged in HBM",
+        "variant": {"fused_adam": model.fuse_optimizer, "keep_grads": model.keep_grads,
+                    "row_pipe": os.environ.get("KGE_ROW_PIPE", "0")},
         "config": {"workload": "RotatE FB15k-shape train_step (fused score+self-adv loss+bwd, dense Adam)",
                    "entities": E, "relations": R, "hidden_dim": D, "batch_per_gpu": B, "global_batch": B * world,
                    "negatives": NNEG, "adversarial_temperature": TEMP, "gamma": GAMMA,

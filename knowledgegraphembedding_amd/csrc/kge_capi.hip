@@ -233,6 +233,11 @@ int run_grad(const kge_model_desc* m, const Geom& geo, int mode, const int64_t* 
   ea.q = w.q; ea.ent_contrib = w.ent_contrib; ea.reg3 = 3.f * reg; ea.reg_partial = w.reg_partial;
   ea.grad_ent = grad_entity;
   ea.write_grad = write_grad;
+  static const int ent_minw = [] {
+    const char* e = getenv("KGE_ENT_MINW");
+    return e ? atoi(e) : 3;  // measured: 4 waves/SIMD spills and runs slower
+  }();
+  ea.minw = ent_minw;
   ea.adam = adam_t(adam ? &adam->entity : nullptr);
   ea.adamk = ak;
   st = launch_status(op.entity(mode, geo.vec, geo.ns, ea, s));

@@ -77,6 +77,7 @@ struct EntArgs {
   float* reg_partial;   // [E] Σ|x|^3 per row (when reg3 != 0)
   float* grad_ent;
   int write_grad;       // store grad_ent (unless the fused optimizer asks not to)
+  int minw;             // k_entity variant: min waves/SIMD the register budget targets (3 or 4)
   AdamT adam;           // fused optimizer step (adam.p == null: none)
   AdamK adamk;
 };

@@ -92,6 +92,8 @@ class KGEModel(nn.Module):
         # leave the dense gradients in .grad after a fused train_step, as
         # loss.backward() does in the reference; False skips those writes
         self.keep_grads = True
+        # apply a KGEAdam update inside the gradient passes (kge_train_step)
+        self.fuse_optimizer = True
 
     # ------------------------------------------------------------------ helpers
     def _host_scalars(self):
@@ -204,7 +206,7 @@ class KGEModel(nn.Module):
         g, rng = self._host_scalars()
         ge, gr, gm, losses = self._grad_buffers()
         adam = None
-        if optimizer is not None and hasattr(optimizer, 'prepare_fused'):
+        if optimizer is not None and self.fuse_optimizer and hasattr(optimizer, 'prepare_fused'):
             adam = optimizer.prepare_fused(self.entity_embedding, self.relation_embedding, self._modulus(),
                                            write_grad=self.keep_grads)
         ops.train_step_grads(
