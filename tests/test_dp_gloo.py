@@ -1,0 +1,114 @@
+"""Data-parallel training logic (knowledgegraphembedding_amd.distributed) with
+world_size 2 over gloo on CPU: two ranks, each with half of a global batch,
+must reproduce the single-process loss and gradients of the whole batch
+(model.py:268-301 semantics: the subsampling normaliser Σw is global).
+
+On CPU the per-rank fused kernel is replaced by the oracle's autograd of the
+same per-rank objective (this file is test infrastructure); everything the DP
+layer itself does — Σw all-reduce, gradient + loss all-reduce, loss
+recomposition, regularisation counted once — runs for real.
+"""
+import os
+import socket
+from argparse import Namespace
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from knowledgegraphembedding_amd import KGEModel, synth
+from knowledgegraphembedding_amd import distributed as kdist
+from oracle import kge_oracle as O
+
+E, R, D, B, N, GAMMA = 60, 5, 8, 8, 6, 12.0
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _make_model(name):
+    torch.manual_seed(0)
+    de, dr = {"RotatE": (True, False), "ComplEx": (True, True), "TransE": (False, False),
+              "DistMult": (False, False), "pRotatE": (False, False)}[name]
+    return KGEModel(name, E, R, D, GAMMA, de, dr)
+
+
+def oracle_rank_grads(model, pos, neg, w, mode, args, weight_sum=None, uni_batch=0, optimizer=None):
+    """Per-rank objective: the rank's share of the global loss."""
+    name = model.model_name
+    ent = model.entity_embedding.detach().clone().requires_grad_(True)
+    rel = model.relation_embedding.detach().clone().requires_grad_(True)
+    mod = model.modulus.detach().clone().requires_grad_(True) if name == "pRotatE" else None
+    g, rng = model.gamma.item(), model.embedding_range.item()
+    s_neg = O.forward(name, ent, rel, mod, (pos, neg), mode, g, rng)
+    if args.negative_adversarial_sampling:
+        neg_term = (torch.softmax(s_neg * args.adversarial_temperature, 1).detach()
+                    * torch.nn.functional.logsigmoid(-s_neg)).sum(1)
+    else:
+        neg_term = torch.nn.functional.logsigmoid(-s_neg).mean(1)
+    pos_term = torch.nn.functional.logsigmoid(O.forward(name, ent, rel, mod, pos, "single", g, rng)).squeeze(1)
+    if args.uni_weight:
+        pl, nl = -pos_term.sum() / uni_batch, -neg_term.sum() / uni_batch
+    else:
+        pl, nl = -(w * pos_term).sum() / weight_sum[0], -(w * neg_term).sum() / weight_sum[0]
+    loss = (pl + nl) / 2
+    reg = torch.zeros(())
+    if args.regularization != 0.0:
+        reg = args.regularization * (ent.norm(p=3) ** 3 + rel.norm(p=3).norm(p=3) ** 3)
+        loss = loss + reg
+    loss.backward()
+    model.entity_embedding.grad = ent.grad
+    model.relation_embedding.grad = rel.grad
+    if mod is not None:
+        model.modulus.grad = mod.grad
+    return torch.stack([pl.detach(), nl.detach(), loss.detach(), reg.detach()]).float()
+
+
+def _worker(rank, world, port, name, adv, uni, reg, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    model = _make_model(name)
+    model.compute_train_grads = lambda *a, **k: oracle_rank_grads(model, *a, **k)
+    pos, neg, w = synth.kge_batch(3, B, N, E, R)
+    sl = slice(rank * B // world, (rank + 1) * B // world)
+    args = Namespace(negative_adversarial_sampling=adv, adversarial_temperature=0.8, uni_weight=uni,
+                     regularization=reg, dp_group=dist.group.WORLD)
+    losses = kdist.dp_train_grads(model, torch.from_numpy(pos[sl]), torch.from_numpy(neg[sl]),
+                                  torch.from_numpy(w[sl]), "tail-batch", args)
+    res = [losses.numpy(), model.entity_embedding.grad.numpy(), model.relation_embedding.grad.numpy()]
+    if name == "pRotatE":
+        res.append(model.modulus.grad.numpy())
+    out[rank] = res
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("name,adv,uni,reg", [("RotatE", True, False, 0.0), ("ComplEx", False, True, 1e-3),
+                                              ("pRotatE", True, False, 0.0), ("DistMult", True, False, 1e-3)])
+def test_dp_two_ranks_match_global_batch(name, adv, uni, reg):
+    world = 2
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_worker, args=(world, _free_port(), name, adv, uni, reg, out), nprocs=world, join=True)
+    model = _make_model(name)
+    pos, neg, w = synth.kge_batch(3, B, N, E, R)
+    log, ge, gr, gm = O.train_grads(name, model.entity_embedding.detach(), model.relation_embedding.detach(),
+                                    model.modulus.detach() if name == "pRotatE" else None, torch.from_numpy(pos),
+                                    torch.from_numpy(neg), torch.from_numpy(w), "tail-batch", adversarial=adv,
+                                    temperature=0.8, uni_weight=uni, regularization=reg,
+                                    gamma=model.gamma.item(), erange=model.embedding_range.item())
+    ref_losses = np.array([log["positive_sample_loss"], log["negative_sample_loss"], log["loss"],
+                           log.get("regularization", 0.0)])
+    for rank in range(world):
+        losses, g_e, g_r = out[rank][:3]
+        np.testing.assert_allclose(losses, ref_losses, rtol=1e-5, atol=1e-6)
+        np.testing.assert_allclose(g_e, ge.numpy(), rtol=1e-4, atol=1e-6 * np.abs(ge.numpy()).max())
+        np.testing.assert_allclose(g_r, gr.numpy(), rtol=1e-4, atol=1e-6 * np.abs(gr.numpy()).max())
+        if name == "pRotatE":
+            np.testing.assert_allclose(out[rank][3], gm.numpy(), rtol=1e-4)
