@@ -172,10 +172,11 @@ def filtered_ranks(name, ent, rel, modulus, triples, all_true_triples, mode, gam
       rank_count    1 + #{unfiltered e != true : s_e > s_true} (strict count, tie-free definition)
       ties          #{unfiltered e != true : s_e == s_true}
       margin64      min over unfiltered e != true of |s_e - s_true| recomputed in float64
+      score64       s_true in float64
     """
     all_true_set = set(map(tuple, np.asarray(all_true_triples).tolist()))
     E = ent.shape[0]
-    out = {k: [] for k in ('rank_argsort', 'rank_count', 'ties', 'margin64')}
+    out = {k: [] for k in ('rank_argsort', 'rank_count', 'ties', 'margin64', 'score64')}
     for tr in np.asarray(triples, dtype=np.int64).tolist():
         cand, bias = filtered_candidates(tr, all_true_set, E, mode)
         pos = torch.tensor([tr], dtype=torch.int64)
@@ -193,6 +194,7 @@ def filtered_ranks(name, ent, rel, modulus, triples, all_true_triples, mode, gam
         s64 = forward(name, ent.double(), rel.double(), None if modulus is None else modulus.double(), (pos, negt),
                       mode, gamma, erange)[0].numpy()
         out['margin64'].append(float(np.min(np.abs(s64[keep] - s64[true_id]))) if keep.any() else np.inf)
+        out['score64'].append(float(s64[true_id]))
     return {k: np.asarray(v) for k, v in out.items()}
 
 

@@ -291,9 +291,9 @@ def test_ranks_vs_golden(g_ranks, golden_info):
                 ref = g_ranks[f"{tag}/{name}/{mode}/rank"]
                 orc = O.filtered_ranks(name, torch.from_numpy(ent), torch.from_numpy(rel),
                                        None if mod is None else torch.from_numpy(mod), test, all_true, mode, g, rng)
-                # margin in units of the score tolerance
-                s_scale = np.maximum(1.0, np.abs(orc["margin64"]))
-                clear = (orc["margin64"] > 1e-4 * s_scale * 10) & (ties == 0)
+                # exact-rank claim: every query whose fp64 margin exceeds the fp32
+                # score tolerance 1e-4·max(|s|, 1) and that has no exact tie
+                clear = (orc["margin64"] > 1e-4 * np.maximum(1.0, np.abs(orc["score64"]))) & (ties == 0)
                 mism = (ranks != ref) & clear
                 assert not mism.any(), f"{tag} {name} {mode}: {np.nonzero(mism)[0]} {ranks[mism]} vs {ref[mism]}"
                 report.append((tag, name, mode, int(clear.sum()), int((~clear).sum()),
