@@ -126,7 +126,12 @@ def main():
     dev = torch.device("cuda", local)
     group = None
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        # RCCL ("nccl") over xGMI; KGE_DIST_BACKEND=gloo rehearses N ranks on one GPU
+        backend = os.environ.get("KGE_DIST_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
         group = dist.group.WORLD
 
     torch.manual_seed(0)

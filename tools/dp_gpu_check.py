@@ -1,0 +1,59 @@
+#!/usr/bin/env python3
+"""Rehearse the data-parallel path on one GPU: N ranks (gloo, all on cuda:0),
+each running the HIP kernels on its shard of a global batch; the reduced loss
+and gradients must match one process running the whole batch.
+
+    python -m torch.distributed.run --nproc-per-node 2 --master-addr 127.0.0.1 \
+        --master-port 29511 tools/dp_gpu_check.py
+Exit status 0 on agreement (fp32 tolerance), 1 otherwise.
+"""
+import os
+import sys
+from argparse import Namespace
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from knowledgegraphembedding_amd import KGEModel, synth  # noqa: E402
+from knowledgegraphembedding_amd.distributed import dp_train_grads  # noqa: E402
+
+
+def main():
+    dist.init_process_group("gloo")
+    rank, world = dist.get_rank(), dist.get_world_size()
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    ok = True
+    for name, de, dr, reg, uni in (("RotatE", True, False, 0.0, False), ("ComplEx", True, True, 1e-4, False),
+                                   ("pRotatE", False, False, 0.0, True)):
+        torch.manual_seed(0)
+        m = KGEModel(name, 2000, 30, 100, 12.0, de, dr).to(dev)
+        B, n = 64 * world, 32
+        pos, neg, w = synth.kge_batch(7, B, n, 2000, 30)
+        args = Namespace(negative_adversarial_sampling=True, adversarial_temperature=1.0, uni_weight=uni,
+                         regularization=reg, dp_group=dist.group.WORLD)
+        sl = slice(rank * B // world, (rank + 1) * B // world)
+        t = lambda x: torch.from_numpy(x).to(dev)  # noqa: E731
+        losses = dp_train_grads(m, t(pos[sl]), t(neg[sl]), t(w[sl]), "tail-batch", args).cpu().numpy()
+        ge, gr = m.entity_embedding.grad.cpu().numpy(), m.relation_embedding.grad.cpu().numpy()
+        args.dp_group = None
+        ref = m.compute_train_grads(t(pos), t(neg), t(w), "tail-batch", args).cpu().numpy()
+        re, rr = m.entity_embedding.grad.cpu().numpy(), m.relation_embedding.grad.cpu().numpy()
+        tol = lambda r: 1e-4 * np.abs(r).max() + 1e-4 * np.abs(r)  # noqa: E731
+        good = (np.all(np.abs(losses - ref) <= 1e-4 * np.maximum(1, np.abs(ref)))
+                and np.all(np.abs(ge - re) <= tol(re)) and np.all(np.abs(gr - rr) <= tol(rr)))
+        ok &= bool(good)
+        if rank == 0:
+            print(f"[dp world={world}] {name}: losses {losses[:3]} vs {ref[:3]}  "
+                  f"max|Δg_ent| {np.abs(ge - re).max():.2e}  {'OK' if good else 'MISMATCH'}", flush=True)
+    flag = torch.tensor([0 if ok else 1])
+    dist.all_reduce(flag)
+    dist.destroy_process_group()
+    sys.exit(int(flag.item() > 0))
+
+
+if __name__ == "__main__":
+    main()
