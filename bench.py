@@ -122,6 +122,8 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if os.environ.get("KGE_DIST_BACKEND", "nccl") != "nccl":
+        local %= torch.cuda.device_count()  # rehearsal: several ranks may share a GPU
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     group = None
