@@ -125,8 +125,9 @@ int kge_score_backward(const kge_model_desc *m, int32_t mode, const int64_t *pos
  *   uni_batch:       the global batch size used for the uni_weight means (0 = batch)
  *   adversarial:     args.negative_adversarial_sampling; temperature = args.adversarial_temperature
  *   regularization:  args.regularization (model.py:290-296); 0 disables
- *   losses_out [4]:  {positive_sample_loss, negative_sample_loss, loss, regularization}
- *                    (device fp32; the reference's log dict, model.py:305-310)
+ *   losses_out [5]:  {positive_sample_loss, negative_sample_loss, loss, regularization,
+ *                     error flag} (device fp32; the reference's log dict, model.py:305-310,
+ *                    plus a copy of *err_flag so one read-back serves both)
  *   grad_* overwritten densely, as in kge_score_backward.
  */
 size_t kge_train_workspace_bytes(const kge_model_desc *m, int64_t batch, int64_t nneg);

@@ -431,6 +431,7 @@ static int train_impl(const kge_model_desc* m, int32_t mode, const int64_t* pos,
   fa.uni_weight = uni_weight ? 1 : 0;
   fa.uni_n = (float)ub;
   fa.losses = losses_out;
+  fa.err = err_flag;
   return run_grad(m, geo, mode, pos, neg, nneg, batch, nneg, ra, w, grad_entity, grad_relation,
                   m->model == KGE_PROTATE ? grad_modulus : nullptr, regularization, fa, adam, err_flag, s);
 }

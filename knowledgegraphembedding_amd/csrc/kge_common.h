@@ -44,6 +44,7 @@ struct FinArgs {
   float regularization;
   float* losses;             // [4]
   float* grad_modulus;       // nullable
+  const int32_t* err;        // device error flag, copied to losses[4]
   AdamT adam;                // fused optimizer step of the pRotatE modulus (adam.p == null: none)
   AdamK adamk;
 };

@@ -221,6 +221,9 @@ __global__ __launch_bounds__(1024) void k_finalize(FinArgs a) {
       a.losses[1] = neg_loss;
       a.losses[2] = loss;
       a.losses[3] = reg;
+      // the device error flag rides along, so the caller's one read-back of
+      // the losses also tells it whether any index was out of range
+      a.losses[4] = a.err ? (float)__hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.f;
     }
     if (a.grad_modulus) a.grad_modulus[0] = tot[5];
     if (a.adam.p) {  // pRotatE modulus, fused optimizer step

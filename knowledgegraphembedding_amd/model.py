@@ -191,15 +191,15 @@ class KGEModel(nn.Module):
             ge = torch.empty_like(self.entity_embedding, memory_format=torch.contiguous_format)
             gr = torch.empty_like(self.relation_embedding, memory_format=torch.contiguous_format)
             gm = torch.empty(1, 1, device=dev) if self.model_name == 'pRotatE' else None
-            losses = torch.empty(4, device=dev)
+            losses = torch.empty(5, device=dev)  # 4 losses + the device error flag
             self._grad_bufs = bufs = (ge, gr, gm, losses)
         return bufs
 
     def compute_train_grads(self, positive_sample, negative_sample, subsampling_weight, mode, args,
                             weight_sum=None, uni_batch=0, optimizer=None):
         """Fused forward + self-adversarial loss + backward (model.py:268-301).
-        Writes dense .grad tensors; returns the device [4] loss vector
-        (positive_sample_loss, negative_sample_loss, loss, regularization).
+        Writes dense .grad tensors; returns the device [5] vector
+        (positive_sample_loss, negative_sample_loss, loss, regularization, error flag).
         With a KGEAdam `optimizer` the Adam update is applied inside the same
         gradient passes (the optimizer's next step() then skips these tables)."""
         dev = ops._require_device(self.entity_embedding)
@@ -252,8 +252,9 @@ class KGEModel(nn.Module):
 
         optimizer.step()
 
-        vals = losses.cpu().tolist()
-        ops.raise_on_device_error(dev)
+        vals = losses.cpu().tolist()  # the step's only device→host sync
+        if vals[4] != 0.0:  # device error flag (out-of-range index), copied by the kernels
+            ops.raise_on_device_error(dev)
         log = {}
         if args.regularization != 0.0:
             log['regularization'] = vals[3]

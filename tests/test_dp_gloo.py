@@ -68,7 +68,7 @@ def oracle_rank_grads(model, pos, neg, w, mode, args, weight_sum=None, uni_batch
     model.relation_embedding.grad = rel.grad
     if mod is not None:
         model.modulus.grad = mod.grad
-    return torch.stack([pl.detach(), nl.detach(), loss.detach(), reg.detach()]).float()
+    return torch.stack([pl.detach(), nl.detach(), loss.detach(), reg.detach(), torch.zeros(())]).float()
 
 
 def _worker(rank, world, port, name, adv, uni, reg, out):
@@ -107,7 +107,8 @@ def test_dp_two_ranks_match_global_batch(name, adv, uni, reg):
                            log.get("regularization", 0.0)])
     for rank in range(world):
         losses, g_e, g_r = out[rank][:3]
-        np.testing.assert_allclose(losses, ref_losses, rtol=1e-5, atol=1e-6)
+        np.testing.assert_allclose(losses[:4], ref_losses, rtol=1e-5, atol=1e-6)
+        assert losses[4] == 0.0  # error flag
         np.testing.assert_allclose(g_e, ge.numpy(), rtol=1e-4, atol=1e-6 * np.abs(ge.numpy()).max())
         np.testing.assert_allclose(g_r, gr.numpy(), rtol=1e-4, atol=1e-6 * np.abs(gr.numpy()).max())
         if name == "pRotatE":
