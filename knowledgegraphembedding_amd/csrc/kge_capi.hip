@@ -187,22 +187,29 @@ int run_grad(const kge_model_desc* m, const Geom& geo, int mode, const int64_t* 
   hipStream_t ss = sd ? sd->s : s;
   int st;
 
-  // fork: the occurrence CSR needs only the batch indices
+  // fork point: the occurrence CSR needs only the batch indices (recorded
+  // before anything else is queued, so the side stream never waits for the
+  // row pass)
+  if (sd) hipEventRecord(sd->fork, s);
+
+  // q build + gather loop on the caller's stream, launched first so the GPU
+  // is on the long kernel while the host queues everything else
+  if (timed) g_timer.mark(s);
+  st = launch_status(op.row(mode, geo.vec, geo.ns, 0, ra, lds, s));
+  if (st) return st;
+  if (timed) g_timer.mark(s);
+
   CsrArgs ca;
   ca.pos = pos; ca.neg = neg; ca.neg_stride = neg_stride;
   ca.B = B; ca.n = n; ca.Bn = B * n; ca.E = m->nentity; ca.R = m->nrelation;
   ca.keys = w.keys; ca.cnt = w.cnt; ca.off = w.off; ca.tmp = w.tmp; ca.occ = w.occ; ca.err = err;
-  if (sd) {
-    hipEventRecord(sd->fork, s);
-    hipStreamWaitEvent(ss, sd->fork, 0);
-  }
+  if (sd) hipStreamWaitEvent(ss, sd->fork, 0);
   st = launch_status(launch_csr(ca, ss));
   if (st) return st;
   if (sd) hipEventRecord(sd->csr_done, ss);
 
-  // row pass on the caller's stream: q build | gather loop | epilogue
-  if (timed) g_timer.mark(s);
-  st = launch_status(op.row(mode, geo.vec, geo.ns, ra, lds, s));
+  // epilogue (positive score, chain rule)
+  st = launch_status(op.row(mode, geo.vec, geo.ns, 1, ra, lds, s));
   if (st) return st;
   if (timed) g_timer.mark(s);
 
@@ -407,9 +414,9 @@ static int train_impl(const kge_model_desc* m, int32_t mode, const int64_t* pos,
   if (!workspace || workspace_bytes < need) return KGE_ERR_WORKSPACE;
   hipStream_t s = as_stream(stream);
   const float* wsum = weight_sum;
+  float* wsum_out = nullptr;
   if (!uni_weight && !wsum) {
-    st = launch_status(launch_weight_sum(subsampling_weight, batch, w.wsum, s));
-    if (st) return st;
+    wsum_out = w.wsum;  // computed by k_build_q's first block, before k_row reads it
     wsum = w.wsum;
   }
   const int64_t ub = uni_batch > 0 ? uni_batch : batch;
@@ -421,6 +428,7 @@ static int train_impl(const kge_model_desc* m, int32_t mode, const int64_t* pos,
   ra.uni_inv = 1.f / (float)ub;
   ra.sub_w = subsampling_weight;
   ra.w_sum = wsum;
+  ra.wsum_out = wsum_out;
   ra.n_lds = (int)nneg;
   if (nneg > 8192) return KGE_ERR_DIM;
   FinArgs fa;

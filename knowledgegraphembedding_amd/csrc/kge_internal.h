@@ -46,6 +46,7 @@ struct RowArgs {
   float uni_inv;    // 1 / global batch (uni_weight)
   const float* sub_w;
   const float* w_sum;
+  float* wsum_out;    // non-null: k_build_q's block 0 writes Σ sub_w here (= w_sum)
   const float* g_in;  // ROW_GIVEN: dL/dscore [B, n]
   float* g_out;       // ROW_TRAIN: dL/ds_ij [B, n]
   float* q_out;       // [B, Le]
@@ -106,7 +107,7 @@ struct RankArgs {
 
 struct ModelOps {
   int (*score)(int mode, int vec, int ns, const ScoreArgs&, int64_t units, hipStream_t);
-  int (*row)(int mode, int vec, int ns, const RowArgs&, size_t lds, hipStream_t);
+  int (*row)(int mode, int vec, int ns, int stage, const RowArgs&, size_t lds, hipStream_t);
   int (*entity)(int mode, int vec, int ns, const EntArgs&, hipStream_t);
   int (*rank)(int mode, int vec, int ns, const RankArgs&, hipStream_t);
 };

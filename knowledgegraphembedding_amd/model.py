@@ -111,10 +111,18 @@ class KGEModel(nn.Module):
         return self.modulus if self.model_name == 'pRotatE' else None
 
     def desc(self):
+        """The C-ABI model descriptor, rebuilt only when a table moves or is replaced."""
         g, rng = self._host_scalars()
         mod = self._modulus()
-        return ops.make_desc(self.model_name, self.entity_embedding.detach(), self.relation_embedding.detach(), g, rng,
-                             None if mod is None else mod.detach())
+        ent, rel = self.entity_embedding, self.relation_embedding
+        key = (ent.data_ptr(), rel.data_ptr(), None if mod is None else mod.data_ptr(), tuple(ent.shape),
+               tuple(rel.shape), g, rng)
+        cached = getattr(self, '_desc_cache', None)
+        if cached is None or cached[0] != key:
+            d = ops.make_desc(self.model_name, ent.detach(), rel.detach(), g, rng,
+                              None if mod is None else mod.detach())
+            self._desc_cache = cached = (key, d)
+        return cached[1]
 
     # ------------------------------------------------------------------ forward
     def forward(self, sample, mode='single'):

@@ -57,6 +57,7 @@ class _DeviceState:
 
 
 _STATES: dict = {}
+_WS_BYTES: dict = {}  # (dims, counts, B, n) -> kge_train_workspace_bytes
 
 
 def state(dev: torch.device) -> _DeviceState:
@@ -182,7 +183,10 @@ def train_step_grads(desc: _lib.ModelDesc, mode: str, pos: torch.Tensor, neg: to
     w = sub_w.to(dev, dtype=torch.float32, non_blocking=True).contiguous().view(-1)
     B, n = neg.shape
     lib = _lib.load()
-    need = lib.kge_train_workspace_bytes(desc, B, n)
+    key = (desc.entity_dim, desc.relation_dim, desc.nentity, desc.nrelation, B, n)
+    need = _WS_BYTES.get(key)
+    if need is None:
+        need = _WS_BYTES[key] = lib.kge_train_workspace_bytes(desc, B, n)
     st = state(dev)
     ws = st.workspace(need)
     common = (desc, _lib.MODE_IDS[mode], pos.data_ptr(), neg.data_ptr(), B, n, w.data_ptr(), _ptr(weight_sum_dev),
