@@ -61,6 +61,17 @@ int check_model(const kge_model_desc* m, Geom* g) {
   return KGE_OK;
 }
 
+// DistMult / ComplEx scores are <q, e>: ranked on the matrix cores when rows
+// are float4-aligned (KGE_RANK_MFMA=0 forces the VALU scan, for A/B runs).
+bool use_mfma_rank(const kge_model_desc* m) {
+  static const int on = [] {
+    const char* e = getenv("KGE_RANK_MFMA");
+    return e ? atoi(e) : 1;
+  }();
+  return on && (m->model == KGE_DISTMULT || m->model == KGE_COMPLEX) && (m->entity_dim % 4 == 0) &&
+         aligned16(m->entity_embedding);
+}
+
 Consts consts_of(const kge_model_desc* m) {
   Consts c;
   c.gamma = m->gamma;
@@ -487,6 +498,7 @@ size_t kge_rank_workspace_bytes(const kge_model_desc* m, int64_t nq) {
   c.take<int64_t>(nq);
   c.take<int32_t>(nq);
   c.take<int32_t>(nq);
+  if (use_mfma_rank(m)) c.take<uint32_t>(nq * ((m->nentity + 31) / 32));  // filtered-candidate bitmap
   return c.off + 256;
 }
 
@@ -518,7 +530,15 @@ int kge_rank_filtered(const kge_model_desc* m, int32_t mode, const int64_t* quer
   if (e != hipSuccess) return hip_status(e);
   e = hipMemsetAsync(a.eq, 0, sizeof(int32_t) * nq, s);
   if (e != hipSuccess) return hip_status(e);
-  return launch_status(ops_for(m->model).rank(mode, geo.vec, geo.ns, a, s));
+  const bool mfma = use_mfma_rank(m) && nq <= 65535;
+  a.prep_only = mfma ? 1 : 0;
+  st = launch_status(ops_for(m->model).rank(mode, geo.vec, geo.ns, a, s));
+  if (st || !mfma) return st;
+  // bilinear models: S = Q · Eᵀ on the matrix cores (kge_rank_mfma.hip)
+  uint32_t* bits = c.take<uint32_t>(nq * ((m->nentity + 31) / 32));
+  return launch_status(launch_rank_mfma(a.q, m->entity_embedding, nq, m->nentity, m->entity_dim, a.true_id,
+                                        a.s_true, filt_off, filt_ids, bits, a.gt, a.eq, ranks_out, ties_out,
+                                        err_flag, s));
 }
 
 int kge_stage_timer(int32_t command, float* stage_ms_out, int32_t n_out) {

@@ -103,6 +103,7 @@ struct RankArgs {
   int64_t* ranks;
   int32_t* ties;
   int32_t* err;
+  int prep_only;        // launch k_rank_prep only (the MFMA path counts on its own)
 };
 
 struct ModelOps {

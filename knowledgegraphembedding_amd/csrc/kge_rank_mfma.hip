@@ -1,0 +1,227 @@
+// kge_rank_mfma.hip — filtered ranking for the bilinear models (DistMult,
+// ComplEx) as an fp32 MFMA tile (model.py:346-418 with TestDataset's filter,
+// dataloader.py:134-154).
+//
+// Both models score a candidate e as a dot product of the query vector q
+// (DistMult: h∘r or r∘t; ComplEx: the rotated complex vector, [re | im]) with
+// the candidate's stored row, so a block of queries against all entities is
+// S = Q · Eᵀ.  v_mfma_f32_32x32x2_f32 computes exact fp32 as a k-ordered fma
+// chain; the true entity's score comes from the SAME kernel in "gather" mode
+// (B columns = the queries' true rows), so s_true and every candidate score
+// are produced by identical instruction sequences and compare consistently.
+//
+// Tile: 128 queries × 128 candidates per workgroup (4 waves as 2×2, each
+// 64×64 = 2×2 MFMA tiles), K staged through LDS 16 deep, transposed to
+// [k][row] so each lane's A/B operand is one conflict-free ds_read_b32.
+// Epilogue: v_cmp → wave ballot → popcounts per query row, summed in LDS,
+// then one integer atomic per (block, query): exact and order-free.
+#include "kge_common.h"
+
+namespace kge {
+
+namespace {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int BM = 128, BN = 128, BK = 16;
+
+struct MfmaArgs {
+  const float* q;        // [nq, K]
+  const float* ent;      // [E, K]
+  int64_t nq, E;
+  int K;
+  const int64_t* true_id;  // [nq]
+  float* s_true;           // [nq]  gather pass writes, scan pass reads
+  const uint32_t* fbits;   // [nq, W] filtered-candidate bitmap (scan pass)
+  int64_t W;
+  int32_t* gt;             // [nq]
+  int32_t* eq;             // [nq]
+};
+
+// Stage a [rows × BK] slab of row-major [*, K] data into LDS as [BK][128].
+// Thread t loads float4 (row t/4 + 64u, k = (t%4)*4 .. +3).
+__device__ __forceinline__ void stage(float (*dst)[128], const float* __restrict__ src, const int64_t* rows,
+                                      int K, int k0, int t) {
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int r = (t >> 2) + 64 * u;
+    const int kq = (t & 3) * 4;
+    const int64_t row = rows[r];
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (row >= 0) {
+      const float* p = src + row * (int64_t)K + k0 + kq;
+      if (k0 + kq + 3 < K) {
+        v = *reinterpret_cast<const float4*>(p);
+      } else {
+        if (k0 + kq + 0 < K) v.x = p[0];
+        if (k0 + kq + 1 < K) v.y = p[1];
+        if (k0 + kq + 2 < K) v.z = p[2];
+      }
+    }
+    dst[kq + 0][r] = v.x;
+    dst[kq + 1][r] = v.y;
+    dst[kq + 2][r] = v.z;
+    dst[kq + 3][r] = v.w;
+  }
+}
+
+template <bool GATHER>
+__global__ __launch_bounds__(256) void k_rank_mfma(MfmaArgs a) {
+  __shared__ __attribute__((aligned(16))) float As[BK][128];
+  __shared__ __attribute__((aligned(16))) float Bs[BK][128];
+  __shared__ int64_t arow[128], brow[128], tids[128];
+  __shared__ float sts[128];
+  __shared__ int32_t cgt[128], ceq[128];
+  const int t = threadIdx.x, lane = t & 63, w = wave_id();
+  const int wm = w >> 1, wn = w & 1;
+  const int64_t q0 = (int64_t)blockIdx.y * BM;
+  const int64_t e0 = (int64_t)blockIdx.x * BN;
+  if (t < 128) {
+    const int64_t q = q0 + t;
+    arow[t] = (q < a.nq) ? q : -1;
+    const int64_t tid_ = (q < a.nq) ? a.true_id[q] : -1;
+    tids[t] = tid_;
+    if (GATHER) {
+      brow[t] = (tid_ >= 0 && tid_ < a.E) ? tid_ : -1;
+    } else {
+      const int64_t e = e0 + t;
+      brow[t] = (e < a.E) ? e : -1;
+      sts[t] = (q < a.nq) ? a.s_true[q] : 0.f;
+    }
+    cgt[t] = 0;
+    ceq[t] = 0;
+  }
+  __syncthreads();
+
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  const int kh = lane >> 5, li = lane & 31;
+  for (int k0 = 0; k0 < a.K; k0 += BK) {
+    stage(As, a.q, arow, a.K, k0, t);
+    stage(Bs, a.ent, brow, a.K, k0, t);
+    __syncthreads();
+#pragma unroll
+    for (int kk = 0; kk < BK / 2; ++kk) {
+      // k order: (k0 + 2kk) in lanes 0-31, (k0 + 2kk + 1) in lanes 32-63 —
+      // ascending k across the loop, the same in both passes
+      float af[2], bf[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) af[i] = As[2 * kk + kh][wm * 64 + i * 32 + li];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) bf[j] = Bs[2 * kk + kh][wn * 64 + j * 32 + li];
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i], bf[j], acc[i][j], 0, 0, 0);
+    }
+    __syncthreads();
+  }
+
+  // C/D layout: col = lane & 31, row = (reg & 3) + 8 * (reg >> 2) + 4 * (lane >> 5)
+  if (GATHER) {
+    if (wm != wn) return;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * kh;
+        const int n = wn * 64 + i * 32 + li;  // diagonal sub-tile j == i
+        if (m == n && arow[m] >= 0) a.s_true[q0 + m] = acc[i][i][r];
+      }
+    return;
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int n = wn * 64 + j * 32 + li;
+      const int64_t e = brow[n];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * kh;
+        const int64_t q = arow[m];
+        bool ok = (q >= 0) && (e >= 0) && (e != tids[m]);
+        if (ok) {
+          const uint32_t word = a.fbits[q * a.W + (e >> 5)];
+          ok = ((word >> (e & 31)) & 1u) == 0u;  // filtered: bias −1 and the true id, never above
+        }
+        const float s = acc[i][j][r];
+        const float st = sts[m];
+        const uint64_t bg = __ballot(ok && s > st);
+        const uint64_t be = __ballot(ok && s == st);
+        if (lane == 0) {
+          const int m_lo = wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2);
+          const int g0 = __popcll(bg & 0xffffffffull), g1 = __popcll(bg >> 32);
+          const int q0c = __popcll(be & 0xffffffffull), q1c = __popcll(be >> 32);
+          if (g0) atomicAdd(&cgt[m_lo], g0);
+          if (g1) atomicAdd(&cgt[m_lo + 4], g1);
+          if (q0c) atomicAdd(&ceq[m_lo], q0c);
+          if (q1c) atomicAdd(&ceq[m_lo + 4], q1c);
+        }
+      }
+    }
+  __syncthreads();
+  if (t < 128 && arow[t] >= 0) {
+    if (cgt[t]) atomicAdd(&a.gt[q0 + t], cgt[t]);
+    if (ceq[t]) atomicAdd(&a.eq[q0 + t], ceq[t]);
+  }
+}
+
+// filtered-candidate bitmap from the CSR (one thread per filtered id)
+__global__ __launch_bounds__(256) void k_filter_bits(const int64_t* __restrict__ off, const int64_t* __restrict__ ids,
+                                                     int64_t nq, int64_t E, int64_t W, uint32_t* __restrict__ bits,
+                                                     int32_t* err) {
+  const int64_t q = blockIdx.y;
+  if (q >= nq) return;
+  const int64_t b = off[q], e_ = off[q + 1];
+  for (int64_t p = b + (int64_t)blockIdx.x * 256 + threadIdx.x; p < e_; p += (int64_t)gridDim.x * 256) {
+    const int64_t e = ids[p];
+    if (e < 0 || e >= E) {
+      atomicOr(err, KGE_DEVERR_INDEX);
+      continue;
+    }
+    atomicOr(&bits[q * W + (e >> 5)], 1u << (e & 31));
+  }
+}
+
+__global__ __launch_bounds__(256) void k_rank_emit(const int32_t* __restrict__ gt, const int32_t* __restrict__ eq,
+                                                   const int64_t* __restrict__ true_id, int64_t nq,
+                                                   int64_t* __restrict__ ranks, int32_t* __restrict__ ties) {
+  const int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (q >= nq) return;
+  const bool ok = true_id[q] >= 0;
+  ranks[q] = ok ? 1 + (int64_t)gt[q] : 0;
+  if (ties) ties[q] = ok ? eq[q] : 0;
+}
+
+}  // namespace
+
+size_t rank_mfma_extra_bytes(int64_t nq, int64_t E) { return (size_t)nq * (size_t)((E + 31) / 32) * 4 + 256; }
+
+// q, true ids (and the q-prep's s_true slot) come from k_rank_prep.
+int launch_rank_mfma(const float* q, const float* ent, int64_t nq, int64_t E, int K, const int64_t* true_id,
+                     float* s_true, const int64_t* filt_off, const int64_t* filt_ids, uint32_t* bits, int32_t* gt,
+                     int32_t* eq, int64_t* ranks, int32_t* ties, int32_t* err, hipStream_t s) {
+  const int64_t W = (E + 31) / 32;
+  hipError_t he = hipMemsetAsync(bits, 0, (size_t)nq * W * 4, s);
+  if (he != hipSuccess) return (int)he;
+  if (nq > 65535) return -1;
+  hipLaunchKernelGGL(k_filter_bits, dim3(4, (unsigned)nq), dim3(256), 0, s, filt_off, filt_ids, nq, E, W, bits, err);
+  MfmaArgs a;
+  a.q = q; a.ent = ent; a.nq = nq; a.E = E; a.K = K; a.true_id = true_id; a.s_true = s_true;
+  a.fbits = bits; a.W = W; a.gt = gt; a.eq = eq;
+  const unsigned gy = (unsigned)((nq + BM - 1) / BM);
+  hipLaunchKernelGGL(k_rank_mfma<true>, dim3(1, gy), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(k_rank_mfma<false>, dim3((unsigned)((E + BN - 1) / BN), gy), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(k_rank_emit, dim3((unsigned)((nq + 255) / 256)), dim3(256), 0, s, gt, eq, true_id, nq, ranks,
+                     ties);
+  return (int)hipGetLastError();
+}
+
+}  // namespace kge

@@ -1,0 +1,93 @@
+#!/usr/bin/env python3
+"""Filtered-ranking benchmark — BASELINE config 3: DistMult + ComplEx on the
+wn18rr shape (E=40943, R=11) d=500, all 3134 test triples × both directions
+(6268 queries) through KGEModel.rank_queries (kge_rank_filtered).
+
+Synthetic graph: 93,003 true triples (wn18rr's train+valid+test count) drawn
+uniformly; tables U(-range, range).  Reports queries/s, the launch time, and
+the MFMA roofline (2·nq·E·K flops ÷ time vs 157.3 TF fp32 dense).
+Set KGE_RANK_MFMA=0 to time the VALU streaming scan instead.
+
+    python tools/bench_rank.py [--models DistMult ComplEx RotatE] [--reps 3] [--cpu-sample 8]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from knowledgegraphembedding_amd import KGEModel, synth  # noqa: E402
+from knowledgegraphembedding_amd.filters import FilterIndex  # noqa: E402
+
+E, R, NTRUE, NTEST = 40943, 11, 93003, 3134
+FP32_PEAK_TF = 157.3
+DIMS = {"DistMult": (False, False), "ComplEx": (True, True), "RotatE": (True, False), "TransE": (False, False),
+        "pRotatE": (False, False)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--models", nargs="+", default=["DistMult", "ComplEx"])
+    ap.add_argument("-d", "--hidden_dim", type=int, default=500)
+    ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--cpu-sample", type=int, default=0, help="queries timed through the CPU oracle (0: skip)")
+    a = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    h = synth.randint(901, (NTRUE,), E)
+    r = synth.randint(902, (NTRUE,), R)
+    t = synth.randint(903, (NTRUE,), E)
+    true = np.unique(np.stack([h, r, t], 1), axis=0)
+    test = true[synth.randint(904, (NTEST,), len(true))]
+    index = FilterIndex(true, E, R)
+    out = []
+    for name in a.models:
+        de, dr = DIMS[name]
+        torch.manual_seed(0)
+        m = KGEModel(name, E, R, a.hidden_dim, 12.0, de, dr).to(dev)
+        K = m.entity_dim
+        times = []
+        ranks = None
+        for rep in range(a.reps + 1):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            rh, _ = m.rank_queries(test, index, "head-batch")
+            rt, _ = m.rank_queries(test, index, "tail-batch")
+            torch.cuda.synchronize()
+            if rep:
+                times.append(time.perf_counter() - t0)
+            ranks = np.concatenate([rh, rt])
+        dt = min(times)
+        nq = 2 * NTEST
+        flops = 2.0 * nq * E * K
+        res = {"model": name, "hidden_dim": a.hidden_dim, "entity_dim": K, "queries": nq,
+               "seconds": dt, "queries_per_s": nq / dt, "candidate_scores_per_s": nq * E / dt,
+               "tflops": flops / dt / 1e12,
+               "path": ("mfma" if name in ("DistMult", "ComplEx") and os.environ.get("KGE_RANK_MFMA", "1") != "0"
+                        else "valu-scan"),
+               "mrr": float(np.mean(1.0 / ranks))}
+        if res["path"] == "mfma":
+            res["roofline"] = {"bound": "mfma", "achieved": res["tflops"], "peak": FP32_PEAK_TF, "unit": "TFLOP/s",
+                               "frac": res["tflops"] / FP32_PEAK_TF}
+        if a.cpu_sample:
+            from oracle import kge_oracle as O
+            ent = m.entity_embedding.detach().cpu()
+            rel = m.relation_embedding.detach().cpu()
+            mod = m.modulus.detach().cpu() if name == "pRotatE" else None
+            g, rng = m._host_scalars()
+            t0 = time.perf_counter()
+            orc = O.filtered_ranks(name, ent, rel, mod, test[:a.cpu_sample], true, "tail-batch", g, rng)
+            cdt = time.perf_counter() - t0
+            res["cpu_oracle_queries_per_s"] = a.cpu_sample / cdt
+            res["cpu_rank_match"] = int((orc["rank_argsort"] == ranks[NTEST:NTEST + a.cpu_sample]).sum())
+        out.append(res)
+        print(json.dumps(res), flush=True)
+    return out
+
+
+if __name__ == "__main__":
+    main()
