@@ -4,7 +4,7 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 TESTS=${TESTS:-tests}
-timeout -k 10 ${TEST_TIMEOUT:-900} python -m pytest $TESTS -m gpu -q -p no:cacheprovider -rs ${PYTEST_EXTRA:-} > gpurun_out/gpu_tests.log 2>&1
+timeout -k 10 ${TEST_TIMEOUT:-900} python -m pytest $TESTS -m gpu -q -p no:cacheprovider -rs ${PYTEST_K:+-k "$PYTEST_K"} > gpurun_out/gpu_tests.log 2>&1
 rc=$?
 echo "pytest rc=$rc"; tail -40 gpurun_out/gpu_tests.log
 if [ $rc -gt 1 ]; then exit $rc; fi
