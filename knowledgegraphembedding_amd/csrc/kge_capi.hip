@@ -64,12 +64,22 @@ int check_model(const kge_model_desc* m, Geom* g) {
 // DistMult / ComplEx scores are <q, e>: ranked on the matrix cores when rows
 // are float4-aligned (KGE_RANK_MFMA=0 forces the VALU scan, for A/B runs).
 bool use_mfma_rank(const kge_model_desc* m) {
-  static const int on = [] {
-    const char* e = getenv("KGE_RANK_MFMA");
-    return e ? atoi(e) : 1;
-  }();
+  const char* ev = getenv("KGE_RANK_MFMA");  // read per call: ranking launches are few and large
+  const int on = ev ? atoi(ev) : 1;
   return on && (m->model == KGE_DISTMULT || m->model == KGE_COMPLEX) && (m->entity_dim % 4 == 0) &&
          aligned16(m->entity_embedding);
+}
+
+// Register-tiled ranking (k_rank_tile) for the models without an MFMA form,
+// and for the bilinear ones when KGE_RANK_MFMA=0.  Needs the reduction length
+// divisible by 4 (float4 staging); KGE_RANK_TILE=0 selects the per-pair
+// wave-reduction scan instead.
+bool use_tile_rank(const kge_model_desc* m) {
+  const char* ev = getenv("KGE_RANK_TILE");
+  const int on = ev ? atoi(ev) : 1;
+  const bool cplx = (m->model == KGE_ROTATE || m->model == KGE_COMPLEX);
+  const int K = cplx ? m->entity_dim / 2 : m->entity_dim;
+  return on && !use_mfma_rank(m) && (K % 4 == 0) && aligned16(m->entity_embedding);
 }
 
 Consts consts_of(const kge_model_desc* m) {
@@ -498,7 +508,7 @@ size_t kge_rank_workspace_bytes(const kge_model_desc* m, int64_t nq) {
   c.take<int64_t>(nq);
   c.take<int32_t>(nq);
   c.take<int32_t>(nq);
-  if (use_mfma_rank(m)) c.take<uint32_t>(nq * ((m->nentity + 31) / 32));  // filtered-candidate bitmap
+  if (use_mfma_rank(m) || use_tile_rank(m)) c.take<uint32_t>(nq * ((m->nentity + 31) / 32));  // filtered-candidate bitmap
   return c.off + 256;
 }
 
@@ -531,14 +541,29 @@ int kge_rank_filtered(const kge_model_desc* m, int32_t mode, const int64_t* quer
   e = hipMemsetAsync(a.eq, 0, sizeof(int32_t) * nq, s);
   if (e != hipSuccess) return hip_status(e);
   const bool mfma = use_mfma_rank(m) && nq <= 65535;
-  a.prep_only = mfma ? 1 : 0;
+  const bool tile = !mfma && use_tile_rank(m) && nq <= 65535;
+  a.prep_only = (mfma || tile) ? 1 : 0;
   st = launch_status(ops_for(m->model).rank(mode, geo.vec, geo.ns, a, s));
-  if (st || !mfma) return st;
-  // bilinear models: S = Q · Eᵀ on the matrix cores (kge_rank_mfma.hip)
+  if (st || !(mfma || tile)) return st;
   uint32_t* bits = c.take<uint32_t>(nq * ((m->nentity + 31) / 32));
-  return launch_status(launch_rank_mfma(a.q, m->entity_embedding, nq, m->nentity, m->entity_dim, a.true_id,
-                                        a.s_true, filt_off, filt_ids, bits, a.gt, a.eq, ranks_out, ties_out,
-                                        err_flag, s));
+  if (mfma)  // bilinear models: S = Q · Eᵀ on the matrix cores (kge_rank_mfma.hip)
+    return launch_status(launch_rank_mfma(a.q, m->entity_embedding, nq, m->nentity, m->entity_dim, a.true_id,
+                                          a.s_true, filt_off, filt_ids, bits, a.gt, a.eq, ranks_out, ties_out,
+                                          err_flag, s));
+  st = launch_status(launch_filter_bits(filt_off, filt_ids, nq, m->nentity, bits, err_flag, s));
+  if (st) return st;
+  TileArgs ta;
+  ta.q = a.q; ta.ent = m->entity_embedding; ta.modulus = m->modulus;
+  ta.nq = nq; ta.E = m->nentity; ta.Le = m->entity_dim;
+  ta.K = (m->model == KGE_ROTATE || m->model == KGE_COMPLEX) ? m->entity_dim / 2 : m->entity_dim;
+  ta.c = a.c; ta.true_id = a.true_id; ta.s_true = a.s_true;
+  ta.fbits = bits; ta.W = (m->nentity + 31) / 32; ta.gt = a.gt; ta.eq = a.eq;
+  const ModelOps& ops = ops_for(m->model);
+  st = launch_status(ops.rank_tile(mode, 1, ta, s));
+  if (st) return st;
+  st = launch_status(ops.rank_tile(mode, 0, ta, s));
+  if (st) return st;
+  return launch_status(launch_rank_emit(a.gt, a.eq, a.true_id, nq, ranks_out, ties_out, s));
 }
 
 int kge_stage_timer(int32_t command, float* stage_ms_out, int32_t n_out) {

@@ -106,11 +106,31 @@ struct RankArgs {
   int prep_only;        // launch k_rank_prep only (the MFMA path counts on its own)
 };
 
+// Register-tiled filtered ranking (kge_kernels.inc, k_rank_tile): 64 queries ×
+// 64 candidates per workgroup, the dim-2 reduction done as one sequential sum
+// per (query, candidate) pair.  The gather pass (B columns = the queries' true
+// rows) writes s_true with the same instruction sequence the scan pass uses.
+struct TileArgs {
+  const float* q;          // [nq, Le]  from k_rank_prep ([re | im] for complex rows)
+  const float* ent;        // [E, Le]
+  const float* modulus;    // pRotatE
+  int64_t nq, E;
+  int Le, K;               // K = reduction length (complex: Le / 2)
+  Consts c;
+  const int64_t* true_id;  // [nq]
+  float* s_true;           // [nq]  gather pass writes, scan pass reads
+  const uint32_t* fbits;   // [nq, W] filtered-candidate bitmap
+  int64_t W;
+  int32_t* gt;             // [nq]
+  int32_t* eq;             // [nq]
+};
+
 struct ModelOps {
   int (*score)(int mode, int vec, int ns, const ScoreArgs&, int64_t units, hipStream_t);
   int (*row)(int mode, int vec, int ns, int stage, const RowArgs&, size_t lds, hipStream_t);
   int (*entity)(int mode, int vec, int ns, const EntArgs&, hipStream_t);
   int (*rank)(int mode, int vec, int ns, const RankArgs&, hipStream_t);
+  int (*rank_tile)(int mode, int gather, const TileArgs&, hipStream_t);
 };
 
 ModelOps model_ops_transe();

@@ -202,26 +202,39 @@ __global__ __launch_bounds__(256) void k_rank_emit(const int32_t* __restrict__ g
 
 }  // namespace
 
-size_t rank_mfma_extra_bytes(int64_t nq, int64_t E) { return (size_t)nq * (size_t)((E + 31) / 32) * 4 + 256; }
+int launch_filter_bits(const int64_t* filt_off, const int64_t* filt_ids, int64_t nq, int64_t E, uint32_t* bits,
+                       int32_t* err, hipStream_t s) {
+  const int64_t W = (E + 31) / 32;
+  hipError_t he = hipMemsetAsync(bits, 0, (size_t)nq * W * 4, s);
+  if (he != hipSuccess) return (int)he;
+  if (nq > 65535) return -1;
+  hipLaunchKernelGGL(k_filter_bits, dim3(4, (unsigned)nq), dim3(256), 0, s, filt_off, filt_ids, nq, E, W, bits, err);
+  return (int)hipGetLastError();
+}
+
+int launch_rank_emit(const int32_t* gt, const int32_t* eq, const int64_t* true_id, int64_t nq, int64_t* ranks,
+                     int32_t* ties, hipStream_t s) {
+  hipLaunchKernelGGL(k_rank_emit, dim3((unsigned)((nq + 255) / 256)), dim3(256), 0, s, gt, eq, true_id, nq, ranks,
+                     ties);
+  return (int)hipGetLastError();
+}
 
 // q, true ids (and the q-prep's s_true slot) come from k_rank_prep.
 int launch_rank_mfma(const float* q, const float* ent, int64_t nq, int64_t E, int K, const int64_t* true_id,
                      float* s_true, const int64_t* filt_off, const int64_t* filt_ids, uint32_t* bits, int32_t* gt,
                      int32_t* eq, int64_t* ranks, int32_t* ties, int32_t* err, hipStream_t s) {
   const int64_t W = (E + 31) / 32;
-  hipError_t he = hipMemsetAsync(bits, 0, (size_t)nq * W * 4, s);
-  if (he != hipSuccess) return (int)he;
-  if (nq > 65535) return -1;
-  hipLaunchKernelGGL(k_filter_bits, dim3(4, (unsigned)nq), dim3(256), 0, s, filt_off, filt_ids, nq, E, W, bits, err);
+  int st = launch_filter_bits(filt_off, filt_ids, nq, E, bits, err, s);
+  if (st) return st;
   MfmaArgs a;
   a.q = q; a.ent = ent; a.nq = nq; a.E = E; a.K = K; a.true_id = true_id; a.s_true = s_true;
   a.fbits = bits; a.W = W; a.gt = gt; a.eq = eq;
   const unsigned gy = (unsigned)((nq + BM - 1) / BM);
   hipLaunchKernelGGL(k_rank_mfma<true>, dim3(1, gy), dim3(256), 0, s, a);
   hipLaunchKernelGGL(k_rank_mfma<false>, dim3((unsigned)((E + BN - 1) / BN), gy), dim3(256), 0, s, a);
-  hipLaunchKernelGGL(k_rank_emit, dim3((unsigned)((nq + 255) / 256)), dim3(256), 0, s, gt, eq, true_id, nq, ranks,
-                     ties);
-  return (int)hipGetLastError();
+  st = (int)hipGetLastError();
+  if (st) return st;
+  return launch_rank_emit(gt, eq, true_id, nq, ranks, ties, s);
 }
 
 }  // namespace kge

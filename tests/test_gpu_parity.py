@@ -277,7 +277,15 @@ def test_kge_adam_matches_torch_adam():
 
 
 # ------------------------------------------------------------------ ranking
-def test_ranks_vs_golden(g_ranks, golden_info):
+# default: MFMA tile (DistMult/ComplEx) + register tile (distance models);
+# tile: the register tile for every model; scan: the per-pair wave-reduction scan
+RANK_PATHS = {"default": {}, "tile": {"KGE_RANK_MFMA": "0"}, "scan": {"KGE_RANK_MFMA": "0", "KGE_RANK_TILE": "0"}}
+
+
+@pytest.mark.parametrize("path", list(RANK_PATHS))
+def test_ranks_vs_golden(g_ranks, golden_info, path, monkeypatch):
+    for k, v in RANK_PATHS[path].items():
+        monkeypatch.setenv(k, v)
     report = []
     for kg in golden_info["ranks"]:
         tag, E, R, d, seed = kg["tag"], kg["E"], kg["R"], kg["d"], kg["seed"]

@@ -6,7 +6,8 @@ wn18rr shape (E=40943, R=11) d=500, all 3134 test triples × both directions
 Synthetic graph: 93,003 true triples (wn18rr's train+valid+test count) drawn
 uniformly; tables U(-range, range).  Reports queries/s, the launch time, and
 the MFMA roofline (2·nq·E·K flops ÷ time vs 157.3 TF fp32 dense).
-Set KGE_RANK_MFMA=0 to time the VALU streaming scan instead.
+Set KGE_RANK_MFMA=0 to time the register-tiled VALU kernel instead, and
+KGE_RANK_TILE=0 as well for the per-pair wave-reduction scan.
 
     python tools/bench_rank.py [--models DistMult ComplEx RotatE] [--reps 3] [--cpu-sample 8]
 """
@@ -28,6 +29,16 @@ E, R, NTRUE, NTEST = 40943, 11, 93003, 3134
 FP32_PEAK_TF = 157.3
 DIMS = {"DistMult": (False, False), "ComplEx": (True, True), "RotatE": (True, False), "TransE": (False, False),
         "pRotatE": (False, False)}
+
+
+def rank_path(name, K):
+    """Which kernel kge_rank_filtered picks (kge_capi.hip: use_mfma_rank / use_tile_rank)."""
+    red = K // 2 if name in ("RotatE", "ComplEx") else K
+    if name in ("DistMult", "ComplEx") and os.environ.get("KGE_RANK_MFMA", "1") != "0" and K % 4 == 0:
+        return "mfma"
+    if os.environ.get("KGE_RANK_TILE", "1") != "0" and red % 4 == 0:
+        return "valu-tile"
+    return "valu-scan"
 
 
 def main():
@@ -67,8 +78,8 @@ def main():
         res = {"model": name, "hidden_dim": a.hidden_dim, "entity_dim": K, "queries": nq,
                "seconds": dt, "queries_per_s": nq / dt, "candidate_scores_per_s": nq * E / dt,
                "tflops": flops / dt / 1e12,
-               "path": ("mfma" if name in ("DistMult", "ComplEx") and os.environ.get("KGE_RANK_MFMA", "1") != "0"
-                        else "valu-scan"),
+               "path": rank_path(name, K),
+               "pair_terms_per_s": nq * E * (K // 2 if name in ("RotatE", "ComplEx") else K) / dt,
                "mrr": float(np.mean(1.0 / ranks))}
         if res["path"] == "mfma":
             res["roofline"] = {"bound": "mfma", "achieved": res["tflops"], "peak": FP32_PEAK_TF, "unit": "TFLOP/s",
