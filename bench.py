@@ -14,6 +14,11 @@ batches pre-staged in HBM (the CPU sampler cannot feed this rate; SURVEY §7 v)
 and alternating tail-/head-batch like BidirectionalOneShotIterator.
 Data: synthetic (uniform ids, reference init U(-range, range) tables).
 
+`--workload yago3-10-rowpart` runs BASELINE config 5 instead: RotatE YAGO3-10
+shape (E=123182, R=37) d=1000 -de, b=1024 per GPU, n=1024, with the entity
+table row-partitioned across the ranks (partition.py: reduce-scatter of the
+dense entity gradient to the row owners, shard Adam, all-gather of the rows).
+
 Prints one JSON line (rank 0).  `roofline` is the dominant kernel (the fused
 row pass) timed live with HIP events on its launch stream; `cpu_baseline` is
 the oracle's ATen op chain (the reference's algorithm) on this host.
@@ -36,6 +41,15 @@ from knowledgegraphembedding_amd import KGEAdam, KGEModel, _lib  # noqa: E402
 
 E, R, D, B, NNEG, GAMMA, TEMP = 14951, 1345, 1000, 1024, 256, 24.0, 1.0
 METRIC = "scored (pos+neg) triples/sec, RotatE FB15k d=1000 b=1024 n=256, 1/2/4/8 GPU"
+WORKLOADS = {
+    # BASELINE config 2 (the headline metric; the driver's default)
+    "fb15k": dict(E=14951, R=1345, D=1000, B=1024, NNEG=256, partition=False,
+                  name="RotatE FB15k-shape train_step (fused score+self-adv loss+bwd, dense Adam)"),
+    # BASELINE config 5
+    "yago3-10-rowpart": dict(E=123182, R=37, D=1000, B=1024, NNEG=1024, partition=True,
+                             name="RotatE YAGO3-10-shape train_step, entity rows partitioned over the ranks "
+                                  "(reduce-scatter grads to owners, shard Adam, all-gather rows)"),
+}
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
 
 
@@ -115,9 +129,13 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
+    ap.add_argument("--workload", choices=sorted(WORKLOADS), default="fb15k")
     ap.add_argument("--traffic-json", default=None,
                     help="rocprofv3 PMC summary (tools/pmc_traffic.py output) for roofline.traffic")
     a = ap.parse_args()
+    global E, R, D, B, NNEG
+    wl = WORKLOADS[a.workload]
+    E, R, D, B, NNEG = wl["E"], wl["R"], wl["D"], wl["B"], wl["NNEG"]
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -145,7 +163,14 @@ def main():
     model.keep_grads = os.environ.get("KGE_KEEP_GRADS", "1") == "1"
     args = Namespace(cuda=True, negative_adversarial_sampling=True, adversarial_temperature=TEMP, uni_weight=False,
                      regularization=0.0, dp_group=group)
-    opt = KGEAdam([p for p in model.parameters() if p.requires_grad], lr=1e-4)
+    part = None
+    if wl["partition"] and group is not None:
+        from knowledgegraphembedding_amd.partition import EntityRowPartition
+        part = EntityRowPartition(model, group)
+        params = part.parameters()
+    else:
+        params = [p for p in model.parameters() if p.requires_grad]
+    opt = KGEAdam(params, lr=1e-4)
     it = DeviceBatches(dev, seed=1000 + rank)
 
     for _ in range(a.warmup):
@@ -198,10 +223,10 @@ def main():
         "data": "synthetic (uniform ids, U(-range,range) tables), batches pre-staged in HBM",
         "variant": {"fused_adam": model.fuse_optimizer, "keep_grads": model.keep_grads,
                     "row_pipe": os.environ.get("KGE_ROW_PIPE", "0")},
-        "config": {"workload": "RotatE FB15k-shape train_step (fused score+self-adv loss+bwd, dense Adam)",
+        "config": {"workload": wl["name"],
                    "entities": E, "relations": R, "hidden_dim": D, "batch_per_gpu": B, "global_batch": B * world,
                    "negatives": NNEG, "adversarial_temperature": TEMP, "gamma": GAMMA,
-                   "parallelism": f"dp{world}"},
+                   "parallelism": (f"rowpart{world}" if part is not None else f"dp{world}")},
         "stage_ms": {"build_q": float(stage[0]) / calls, "row_pass": row_ms, "row_epilogue": float(stage[2]) / calls,
                      "csr_join": float(stage[3]) / calls, "entity_pass": float(stage[4]) / calls,
                      "relation_join_finalize": float(stage[5]) / calls,
@@ -211,6 +236,8 @@ def main():
                      "traffic": traffic, "algorithmic_bytes_per_launch": row_bytes,
                      "avg_launch_ms": row_ms},
     }
+    if a.workload != "fb15k":
+        out["metric"] = f"scored (pos+neg) triples/sec, RotatE {a.workload} d={D} b={B} n={NNEG}"
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(cpu_state, budget_s=a.cpu_budget)
     if rank == 0:

@@ -248,8 +248,12 @@ class KGEModel(nn.Module):
         negative_sample = negative_sample.to(dev, non_blocking=True)
         subsampling_weight = subsampling_weight.to(dev, non_blocking=True)
 
+        part = getattr(model, 'row_partition', None)
         dp = getattr(args, 'dp_group', None)
-        if dp is not None:
+        if part is not None:
+            # row-partitioned entity table (partition.py): reduce-scatter to the owners
+            losses = part.train_grads(model, positive_sample, negative_sample, subsampling_weight, mode, args)
+        elif dp is not None:
             from .distributed import dp_train_grads
             losses = dp_train_grads(model, positive_sample, negative_sample, subsampling_weight, mode, args)
         else:
@@ -259,6 +263,8 @@ class KGEModel(nn.Module):
                                                optimizer=optimizer)
 
         optimizer.step()
+        if part is not None:
+            part.gather()  # owners' updated rows → every replica
 
         vals = losses.cpu().tolist()  # the step's only device→host sync
         if vals[4] != 0.0:  # device error flag (out-of-range index), copied by the kernels

@@ -1,0 +1,151 @@
+"""Row-partitioned entity table for YAGO3-10-scale entity counts (BASELINE
+config 5: RotatE YAGO3-10 d=1000 n=1024 over 8 ranks).
+
+The reference is single-device and keeps the whole table in one
+``nn.Embedding``-like parameter (model.py:45-53).  Here each rank OWNS a
+contiguous row range ("shard") of the entity table together with its Adam
+moments, so the optimizer reads and writes 1/world of the table per rank:
+
+  rank r owns rows [r·S, (r+1)·S), S = ceil(E / world) (the last shard padded)
+
+One training step (same maths as the single-device step on the global batch):
+
+  1. the fused kernel runs on the rank's own positives and negatives against
+     a gathered replica of the whole table (the negative rows the rank
+     sampled; with 1024×1024 draws per rank over 123 k rows every row is hit
+     with probability 1 − e^-8.5, so the sampled-row gather IS a full-table
+     all-gather);
+  2. the dense entity gradient is REDUCE-SCATTERED (SUM) to the owners — each
+     rank receives only its shard's summed gradient;
+  3. relation/modulus gradients and the loss partials are all-reduced, Σw is
+     all-reduced before the kernel (global loss normaliser, model.py:285-286);
+  4. each rank steps Adam on its shard (and on the replicated relation table);
+  5. the updated shards are ALL-GATHERED into the replica for the next step,
+     so after ``train_step`` returns the replica (``model.entity_embedding``)
+     is current and test_step / save_model read it unchanged.
+
+Collective volume per rank and step: one reduce-scatter and one all-gather of
+the (E_pad × d_e) fp32 table, each moving (world−1)/world of it over xGMI.
+The regularisation term reads the full replica, so only rank 0 adds it.
+
+Checkpoints stay in the reference layout: ``gathered_optimizer_state_dict``
+rebuilds the Adam state of the full table, ``load_optimizer_state_dict``
+slices a full-table state back to the shard.
+"""
+from __future__ import annotations
+
+import copy
+
+import torch
+import torch.distributed as dist
+from torch import nn
+
+from .distributed import dp_allreduce_, dp_weight_sum
+
+
+class EntityRowPartition:
+    """Attach to a (replicated-initialised) KGEModel: ``EntityRowPartition(model, group)``.
+
+    After construction ``model.entity_embedding`` is a Parameter viewing the
+    gathered replica; the trainable tensor is ``self.shard``.  Build the
+    optimizer over ``self.parameters()``.
+    """
+
+    def __init__(self, model, group=None):
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        ent = model.entity_embedding
+        E, d = ent.shape
+        self.nentity, self.dim = E, d
+        self.rows = -(-E // self.world)
+        self.lo = self.rank * self.rows
+        self.hi = min(E, self.lo + self.rows)
+        dev = ent.device
+        self.full = torch.zeros(self.world * self.rows, d, device=dev)
+        self.full[:E].copy_(ent.detach())
+        self.shard = nn.Parameter(self.full[self.lo:self.lo + self.rows].clone())
+        self.grad_full = torch.zeros(self.world * self.rows, d, device=dev)
+        # the kernels read the replica and write the dense gradient straight
+        # into the reduce-scatter input (its padding rows stay zero)
+        model.entity_embedding = nn.Parameter(self.full[:E], requires_grad=ent.requires_grad)
+        rel = model.relation_embedding
+        gm = torch.empty(1, 1, device=dev) if model.model_name == 'pRotatE' else None
+        model._grad_bufs = (self.grad_full[:E], torch.empty_like(rel, memory_format=torch.contiguous_format), gm,
+                            torch.empty(5, device=dev))
+        model.fuse_optimizer = False  # Adam runs on the shard, not on the replica the kernel reads
+        model.row_partition = self
+        self.model = model
+
+    # ------------------------------------------------------------ parameters
+    def parameters(self):
+        """Trainable tensors in the reference's order (entity, relation[, modulus])."""
+        m = self.model
+        out = [self.shard, m.relation_embedding]
+        if m.model_name == 'pRotatE':
+            out.append(m.modulus)
+        return [p for p in out if p.requires_grad]
+
+    def gather(self) -> None:
+        """Refresh the replica from every rank's shard (all-gather)."""
+        dist.all_gather_into_tensor(self.full, self.shard.detach(), group=self.group)
+
+    def reload_from_replica(self) -> None:
+        """After writing the replica (load_state_dict), take this rank's rows back."""
+        with torch.no_grad():
+            self.shard.copy_(self.full[self.lo:self.lo + self.rows])
+
+    # -------------------------------------------------------------- training
+    def train_grads(self, model, positive_sample, negative_sample, subsampling_weight, mode, args):
+        """Fused per-rank gradients, reduce-scatter to the owners; returns the global [5] loss vector."""
+        group = self.group
+        B = positive_sample.shape[0]
+        wsum = None if args.uni_weight else dp_weight_sum(subsampling_weight, group)
+        local_args = args
+        if self.rank != 0 and args.regularization != 0.0:
+            local_args = copy.copy(args)
+            local_args.regularization = 0.0
+        losses = model.compute_train_grads(positive_sample, negative_sample, subsampling_weight, mode, local_args,
+                                           weight_sum=wsum, uni_batch=B * self.world)
+        if self.shard.grad is None or self.shard.grad.shape != self.shard.shape:
+            self.shard.grad = torch.empty_like(self.shard)
+        dist.reduce_scatter_tensor(self.shard.grad, self.grad_full, op=dist.ReduceOp.SUM, group=group)
+        model.entity_embedding.grad = None  # the replica is not optimised; its gradient went to the owners
+        rest = [model.relation_embedding.grad]
+        if model.model_name == 'pRotatE' and model.modulus.grad is not None:
+            rest.append(model.modulus.grad)
+        dp_allreduce_(rest + [losses], group)
+        losses[2] = (losses[0] + losses[1]) / 2 + losses[3]
+        return losses
+
+    # ------------------------------------------------------------ checkpoints
+    def _gather_rows(self, t: torch.Tensor) -> torch.Tensor:
+        out = torch.empty(self.world * self.rows, self.dim, device=t.device, dtype=t.dtype)
+        dist.all_gather_into_tensor(out, t.contiguous(), group=self.group)
+        return out[:self.nentity]
+
+    def gathered_optimizer_state_dict(self, optimizer) -> dict:
+        """The optimizer's state_dict with the shard's Adam moments gathered to
+        full-table tensors — the layout a replicated Adam over
+        (entity, relation[, modulus]) would save (run.py:93-120).  Collective."""
+        sd = optimizer.state_dict()
+        st = sd['state'].get(0)
+        if st is not None:
+            st = dict(st)
+            for k in ('exp_avg', 'exp_avg_sq'):
+                st[k] = self._gather_rows(st[k])
+            sd['state'] = dict(sd['state'])
+            sd['state'][0] = st
+        return sd
+
+    def load_optimizer_state_dict(self, optimizer, sd: dict) -> None:
+        """Load a full-table optimizer state (reference layout) into the shard optimizer."""
+        sd = copy.deepcopy(sd)
+        st = sd['state'].get(0)
+        if st is not None:
+            for k in ('exp_avg', 'exp_avg_sq'):
+                full = st[k]
+                part = torch.zeros(self.rows, self.dim, dtype=full.dtype)
+                part[:self.hi - self.lo] = full[self.lo:self.hi]
+                st[k] = part
+        optimizer.load_state_dict(sd)

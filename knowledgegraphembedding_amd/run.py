@@ -69,6 +69,9 @@ def parse_args(args=None):
     parser.add_argument('--test_log_steps', default=1000, type=int, help='valid/test log every xx steps')
     parser.add_argument('--nentity', type=int, default=0, help='DO NOT MANUALLY SET')
     parser.add_argument('--nrelation', type=int, default=0, help='DO NOT MANUALLY SET')
+    parser.add_argument('--row_partition', action='store_true',
+                        help='multi-GPU only: each rank owns 1/world of the entity rows and their Adam state '
+                             '(reduce-scatter of gradients, all-gather of rows; partition.py)')
     return parser.parse_args(args)
 
 
@@ -90,14 +93,16 @@ def _json_args(args):
     return {k: v for k, v in vars(args).items() if not k.startswith('dp_')}
 
 
-def save_model(model, optimizer, save_variable_list, args):
-    '''config.json + checkpoint + entity/relation_embedding.npy (run.py:93-120).'''
+def save_model(model, optimizer, save_variable_list, args, optimizer_state=None):
+    '''config.json + checkpoint + entity/relation_embedding.npy (run.py:93-120).
+    `optimizer_state` overrides optimizer.state_dict() (the row-partitioned
+    trainer passes its state gathered to the full-table layout).'''
     with open(os.path.join(args.save_path, 'config.json'), 'w') as fjson:
         json.dump(_json_args(args), fjson)
     torch.save({
         **save_variable_list,
         'model_state_dict': model.state_dict(),
-        'optimizer_state_dict': optimizer.state_dict()},
+        'optimizer_state_dict': optimizer.state_dict() if optimizer_state is None else optimizer_state},
         os.path.join(args.save_path, 'checkpoint')
     )
     np.save(os.path.join(args.save_path, 'entity_embedding'), model.entity_embedding.detach().cpu().numpy())
@@ -217,6 +222,21 @@ def main(args):
         import torch.distributed as dist
         for p in kge_model.parameters():
             dist.broadcast(p.data, src=0)
+    part = None
+    if getattr(args, 'row_partition', False):
+        if args.dp_group is None:
+            logging.info('--row_partition ignored: one process (launch with torchrun for a partitioned table)')
+        else:
+            from .partition import EntityRowPartition
+            part = EntityRowPartition(kge_model, args.dp_group)
+            logging.info('Entity rows partitioned: rank %d owns [%d, %d)' % (rank, part.lo, part.hi))
+
+    def trainable():
+        return part.parameters() if part is not None else filter(lambda p: p.requires_grad, kge_model.parameters())
+
+    def optimizer_state():
+        # collective under --row_partition: every rank calls it, rank 0 writes
+        return part.gathered_optimizer_state_dict(optimizer) if part is not None else None
 
     if args.do_train:
         train_dataloader_head = DataLoader(
@@ -229,7 +249,7 @@ def main(args):
             collate_fn=TrainDataset.collate_fn)
         train_iterator = BidirectionalOneShotIterator(train_dataloader_head, train_dataloader_tail)
         current_learning_rate = args.learning_rate
-        optimizer = KGEAdam(filter(lambda p: p.requires_grad, kge_model.parameters()), lr=current_learning_rate)
+        optimizer = KGEAdam(trainable(), lr=current_learning_rate)
         warm_up_steps = args.warm_up_steps if args.warm_up_steps else args.max_steps // 2
 
     if args.init_checkpoint:
@@ -238,10 +258,15 @@ def main(args):
                                 weights_only=True)
         init_step = checkpoint['step']
         kge_model.load_state_dict(checkpoint['model_state_dict'])
+        if part is not None:
+            part.reload_from_replica()
         if args.do_train:
             current_learning_rate = checkpoint['current_learning_rate']
             warm_up_steps = checkpoint['warm_up_steps']
-            optimizer.load_state_dict(checkpoint['optimizer_state_dict'])
+            if part is not None:
+                part.load_optimizer_state_dict(optimizer, checkpoint['optimizer_state_dict'])
+            else:
+                optimizer.load_state_dict(checkpoint['optimizer_state_dict'])
     else:
         logging.info('Ramdomly Initializing %s Model...' % args.model)
         init_step = 0
@@ -266,12 +291,13 @@ def main(args):
             if step >= warm_up_steps:
                 current_learning_rate = current_learning_rate / 10
                 logging.info('Change learning_rate to %f at step %d' % (current_learning_rate, step))
-                optimizer = KGEAdam(filter(lambda p: p.requires_grad, kge_model.parameters()),
-                                    lr=current_learning_rate)
+                optimizer = KGEAdam(trainable(), lr=current_learning_rate)
                 warm_up_steps = warm_up_steps * 3
-            if step % args.save_checkpoint_steps == 0 and rank == 0:
-                save_model(kge_model, optimizer, {'step': step, 'current_learning_rate': current_learning_rate,
-                                                  'warm_up_steps': warm_up_steps}, args)
+            if step % args.save_checkpoint_steps == 0:
+                osd = optimizer_state()
+                if rank == 0:
+                    save_model(kge_model, optimizer, {'step': step, 'current_learning_rate': current_learning_rate,
+                                                      'warm_up_steps': warm_up_steps}, args, osd)
             if step % args.log_steps == 0:
                 metrics = {}
                 for metric in training_logs[0].keys():
@@ -282,9 +308,10 @@ def main(args):
                 logging.info('Evaluating on Valid Dataset...')
                 metrics = kge_model.test_step(kge_model, valid_triples, all_true_triples, args)
                 log_metrics('Valid', step, metrics)
+        osd = optimizer_state()
         if rank == 0:
             save_model(kge_model, optimizer, {'step': step, 'current_learning_rate': current_learning_rate,
-                                              'warm_up_steps': warm_up_steps}, args)
+                                              'warm_up_steps': warm_up_steps}, args, osd)
 
     if rank != 0:
         return

@@ -1,0 +1,86 @@
+"""Row-partitioned entity table through the HIP kernels: two ranks (gloo, both
+on cuda:0 — the one-GPU box rehearsal of BASELINE config 5), each owning half
+of the entity rows and training on half of a global batch, against
+single-process training of the whole batch on the same GPU.  Tables after two
+KGEAdam steps and the losses must agree to fp32 rounding (the two paths sum
+the per-rank dense gradients in a different order)."""
+import os
+import socket
+from argparse import Namespace
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from knowledgegraphembedding_amd import KGEAdam, KGEModel, synth
+
+pytestmark = pytest.mark.gpu
+
+E, R, D, B, N, GAMMA, LR = 301, 7, 32, 16, 8, 12.0, 1e-2
+DIMS = {"RotatE": (True, False), "pRotatE": (False, False), "ComplEx": (True, True)}
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _model(name):
+    torch.manual_seed(0)
+    de, dr = DIMS[name]
+    return KGEModel(name, E, R, D, GAMMA, de, dr).to("cuda:0")
+
+
+def _batches(dev):
+    out = []
+    for k, mode in enumerate(("tail-batch", "head-batch")):
+        pos, neg, w = synth.kge_batch(40 + k, B, N, E, R)
+        out.append((torch.from_numpy(pos).to(dev), torch.from_numpy(neg).to(dev), torch.from_numpy(w).to(dev), mode))
+    return out
+
+
+def _args(group):
+    return Namespace(cuda=True, negative_adversarial_sampling=True, adversarial_temperature=1.0, uni_weight=False,
+                     regularization=0.0, dp_group=group)
+
+
+def _worker(rank, world, port, name, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from knowledgegraphembedding_amd.partition import EntityRowPartition
+    model = _model(name)
+    part = EntityRowPartition(model)
+    opt = KGEAdam(part.parameters(), lr=LR)
+    sl = slice(rank * B // world, (rank + 1) * B // world)
+    it = iter([(p[sl], n[sl], w[sl], m) for p, n, w, m in _batches("cuda:0")])
+    logs = [KGEModel.train_step(model, opt, it, _args(dist.group.WORLD)) for _ in range(2)]
+    torch.cuda.synchronize()
+    out[rank] = {"logs": logs, "ent": model.entity_embedding.detach().cpu().numpy(),
+                 "rel": model.relation_embedding.detach().cpu().numpy()}
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("name", ["RotatE", "pRotatE"])
+def test_row_partition_two_ranks_on_gpu(name):
+    world = 2
+    out = mp.Manager().dict()
+    mp.spawn(_worker, args=(world, _free_port(), name, out), nprocs=world, join=True)
+    model = _model(name)
+    opt = KGEAdam([p for p in model.parameters() if p.requires_grad], lr=LR)
+    it = iter(_batches("cuda:0"))
+    ref = [KGEModel.train_step(model, opt, it, _args(None)) for _ in range(2)]
+    ent = model.entity_embedding.detach().cpu().numpy()
+    rel = model.relation_embedding.detach().cpu().numpy()
+    for rank in range(world):
+        r = out[rank]
+        np.testing.assert_allclose(r["ent"], ent, rtol=1e-5, atol=2e-6)
+        np.testing.assert_allclose(r["rel"], rel, rtol=1e-5, atol=2e-6)
+        for got, want in zip(r["logs"], ref):
+            for k in ("positive_sample_loss", "negative_sample_loss", "loss"):
+                np.testing.assert_allclose(got[k], want[k], rtol=2e-5)
