@@ -171,7 +171,18 @@ def main():
     else:
         params = [p for p in model.parameters() if p.requires_grad]
     opt = KGEAdam(params, lr=1e-4)
-    it = DeviceBatches(dev, seed=1000 + rank)
+    sampler = os.environ.get("KGE_BENCH_SAMPLER", "staged")
+    if sampler == "device":
+        # end-to-end variant: every batch drawn inside the timed loop by the
+        # device sampler (sampler.py) from a synthetic FB15k-sized train set
+        from knowledgegraphembedding_amd.sampler import DeviceTrainIterator
+        g = torch.Generator().manual_seed(4242)
+        ntrain = 483142  # FB15k train.txt size
+        train = torch.stack([torch.randint(0, E, (ntrain,), generator=g), torch.randint(0, R, (ntrain,), generator=g),
+                             torch.randint(0, E, (ntrain,), generator=g)], 1).numpy()
+        it = DeviceTrainIterator(train, E, R, NNEG, B, dev, seed=1000 + rank)
+    else:
+        it = DeviceBatches(dev, seed=1000 + rank)
 
     for _ in range(a.warmup):
         KGEModel.train_step(model, opt, it, args)
@@ -222,7 +233,7 @@ def main():
         "dtype": "fp32",
         "data": "synthetic (uniform ids, U(-range,range) tables), batches pre-staged in HBM",
         "variant": {"fused_adam": model.fuse_optimizer, "keep_grads": model.keep_grads,
-                    "row_pipe": os.environ.get("KGE_ROW_PIPE", "0")},
+                    "row_pipe": os.environ.get("KGE_ROW_PIPE", "0"), "batches": sampler},
         "config": {"workload": wl["name"],
                    "entities": E, "relations": R, "hidden_dim": D, "batch_per_gpu": B, "global_batch": B * world,
                    "negatives": NNEG, "adversarial_temperature": TEMP, "gamma": GAMMA,

@@ -60,6 +60,7 @@ enum kge_status {
 
 /* Device-side error bits written to *err_flag. */
 #define KGE_DEVERR_INDEX 1
+#define KGE_DEVERR_SAMPLER 2 /* a row's true list left no room within max_draws draws */
 
 /*
  * The parameters of one KGEModel (model.py:22-70).
@@ -226,6 +227,29 @@ int kge_rank_filtered(const kge_model_desc *m, int32_t mode, const int64_t *quer
  */
 #define KGE_TIMER_STAGES 6
 int kge_stage_timer(int32_t command, float *stage_ms_out, int32_t n_out);
+
+/*
+ * Device negative sampler: one training batch as TrainDataset.__getitem__ +
+ * collate_fn build it (dataloader.py:34-66, sampling loop :44-61), for the
+ * triples `batch[0..batch_size)` (ids into `triples`).
+ *   pos_out[i] = triples[batch[i]], w_out[i] = weights[batch[i]]
+ *     (weights = sqrt(1 / (count(h,r) + count(t,-r-1))), dataloader.py:40-42)
+ *   neg_out[i, :] = the first negative_sample_size draws of row i's uniform
+ *     stream over [0, nentity) that are NOT in the row's true list — the true
+ *     heads of (r, t) for head-batch, the true tails of (h, r) for tail-batch
+ *     (dataloader.py:47-56): true_ids[true_off[t] .. + true_len[t]), sorted.
+ * Row i's stream is a splitmix64 sequence keyed by (key, i); the caller
+ * advances `key` every batch.  The reference draws with numpy's global
+ * MT19937, so parity is distributional and bit-exact against
+ * the restatement of this generator in oracle/kge_oracle.py.
+ * A row still short after max_draws draws sets KGE_DEVERR_SAMPLER (the
+ * reference would loop forever) and is zero-padded.
+ */
+int kge_sample_negatives(const int64_t *triples, int64_t ntriples, const int64_t *batch, int64_t batch_size,
+                         int64_t nentity, int64_t negative_sample_size, const int64_t *true_off,
+                         const int32_t *true_len, const int64_t *true_ids, const float *weights, uint64_t key,
+                         int64_t max_draws, int64_t *pos_out, int64_t *neg_out, float *w_out, int32_t *err_flag,
+                         void *stream);
 
 #ifdef __cplusplus
 }

@@ -16,6 +16,7 @@ LIB_PATH = Path(os.environ.get("KGE_HIP_LIB", _PKG / "libkge_hip.so"))
 MODEL_IDS = {"TransE": 0, "DistMult": 1, "ComplEx": 2, "RotatE": 3, "pRotatE": 4}
 MODE_IDS = {"single": 0, "head-batch": 1, "tail-batch": 2}
 DEVERR_INDEX = 1
+DEVERR_SAMPLER = 2
 ERR_HIP_BASE = 1000
 
 
@@ -83,6 +84,8 @@ SIGNATURES = {
     "kge_rank_workspace_bytes": (_SZ, [_DESC, _I64]),
     "kge_rank_filtered": (C.c_int, [_DESC, _I32, _P, _I64, _P, _P, _P, _P, _P, _SZ, _P, _P]),
     "kge_stage_timer": (C.c_int, [_I32, _P, _I32]),
+    "kge_sample_negatives": (C.c_int, [_P, _I64, _P, _I64, _I64, _I64, _P, _P, _P, _P, C.c_uint64, _I64, _P, _P, _P,
+                                       _P, _P]),
 }
 
 _lib = None

@@ -76,6 +76,9 @@ def raise_on_device_error(dev: torch.device) -> None:
         st.err.zero_()
         if v & _lib.DEVERR_INDEX:
             raise IndexError("index out of range in self")  # what index_select raises (model.py:86-146)
+        if v & _lib.DEVERR_SAMPLER:
+            raise RuntimeError("negative sampler: a positive's true heads/tails leave too few candidate "
+                               "entities (the reference's sampling loop would not terminate)")
         raise RuntimeError(f"device error flag {v}")
 
 
@@ -239,3 +242,23 @@ def rank_filtered(desc: _lib.ModelDesc, mode: str, queries: torch.Tensor, filt_o
         "kge_rank_filtered",
     )
     return ranks, ties
+
+
+def sample_negatives(triples: torch.Tensor, batch: torch.Tensor, nentity: int, negative_sample_size: int,
+                     true_off: torch.Tensor, true_len: torch.Tensor, true_ids: torch.Tensor, weights: torch.Tensor,
+                     key: int, max_draws: int, pos_out: torch.Tensor, neg_out: torch.Tensor, w_out: torch.Tensor):
+    """One batch of TrainDataset samples on the device (dataloader.py:34-66); see kge_sample_negatives."""
+    dev = _require_device(triples, batch, true_off, true_len, true_ids, weights, pos_out, neg_out, w_out)
+    B = batch.shape[0]
+    assert pos_out.shape == (B, 3) and neg_out.shape == (B, negative_sample_size) and w_out.shape == (B,)
+    for t, dt in ((triples, torch.int64), (batch, torch.int64), (true_off, torch.int64), (true_len, torch.int32),
+                  (true_ids, torch.int64), (weights, torch.float32), (pos_out, torch.int64),
+                  (neg_out, torch.int64), (w_out, torch.float32)):
+        if t.dtype != dt or not t.is_contiguous():
+            raise ValueError(f"sample_negatives: expected a contiguous {dt} tensor, got {t.dtype}")
+    lib = _lib.load()
+    _lib.check(lib.kge_sample_negatives(triples.data_ptr(), triples.shape[0], batch.data_ptr(), B, int(nentity),
+                                        int(negative_sample_size), true_off.data_ptr(), true_len.data_ptr(),
+                                        true_ids.data_ptr(), weights.data_ptr(), int(key) & (2 ** 64 - 1),
+                                        int(max_draws), pos_out.data_ptr(), neg_out.data_ptr(), w_out.data_ptr(),
+                                        state(dev).err.data_ptr(), _stream(dev)), "kge_sample_negatives")

@@ -72,6 +72,9 @@ def parse_args(args=None):
     parser.add_argument('--row_partition', action='store_true',
                         help='multi-GPU only: each rank owns 1/world of the entity rows and their Adam state '
                              '(reduce-scatter of gradients, all-gather of rows; partition.py)')
+    parser.add_argument('--device_sampler', action='store_true',
+                        help='build training batches on the GPU (sampler.py) instead of the CPU TrainDataset '
+                             'workers: same sampling semantics, a different random stream')
     return parser.parse_args(args)
 
 
@@ -238,7 +241,12 @@ def main(args):
         # collective under --row_partition: every rank calls it, rank 0 writes
         return part.gathered_optimizer_state_dict(optimizer) if part is not None else None
 
-    if args.do_train:
+    if args.do_train and getattr(args, 'device_sampler', False):
+        from .sampler import DeviceTrainIterator
+        train_iterator = DeviceTrainIterator(train_triples, nentity, nrelation, args.negative_sample_size,
+                                             args.batch_size, kge_model.entity_embedding.device,
+                                             seed=torch.initial_seed() + rank)
+    elif args.do_train:
         train_dataloader_head = DataLoader(
             TrainDataset(train_triples, nentity, nrelation, args.negative_sample_size, 'head-batch'),
             batch_size=args.batch_size, shuffle=True, num_workers=max(1, args.cpu_num // 2),
@@ -248,6 +256,7 @@ def main(args):
             batch_size=args.batch_size, shuffle=True, num_workers=max(1, args.cpu_num // 2),
             collate_fn=TrainDataset.collate_fn)
         train_iterator = BidirectionalOneShotIterator(train_dataloader_head, train_dataloader_tail)
+    if args.do_train:
         current_learning_rate = args.learning_rate
         optimizer = KGEAdam(trainable(), lr=current_learning_rate)
         warm_up_steps = args.warm_up_steps if args.warm_up_steps else args.max_steps // 2

@@ -203,3 +203,80 @@ def metrics_from_ranks(ranks):
     logs = [{'MRR': 1.0 / r, 'MR': float(r), 'HITS@1': 1.0 if r <= 1 else 0.0, 'HITS@3': 1.0 if r <= 3 else 0.0,
              'HITS@10': 1.0 if r <= 10 else 0.0} for r in np.asarray(ranks).tolist()]
     return {k: sum(l[k] for l in logs) / len(logs) for k in logs[0]}
+
+
+# --------------------------------------------------------------- sampler
+# The device sampler (kge_sample_negatives) restated.  Semantics follow
+# TrainDataset.__getitem__ (dataloader.py:34-61): uniform draws over
+# [0, nentity), true heads of (r, t) / true tails of (h, r) rejected, the
+# first n survivors kept in draw order; weights dataloader.py:40-42.  The
+# random stream is the build's (splitmix64 per batch row), not numpy's.
+_M64 = np.uint64(0xFFFFFFFFFFFFFFFF)
+
+
+def _mix64_np(z):
+    z = np.asarray(z, dtype=np.uint64)
+    with np.errstate(over='ignore'):
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+    return z ^ (z >> np.uint64(31))
+
+
+def _mulhi_small(x, E: int):
+    """floor(x * E / 2^64) for uint64 x and E < 2^31, exactly."""
+    e = np.uint64(E)
+    lo = x & np.uint64(0xFFFFFFFF)
+    hi = x >> np.uint64(32)
+    with np.errstate(over='ignore'):
+        return ((hi * e + ((lo * e) >> np.uint64(32))) >> np.uint64(32)).astype(np.int64)
+
+
+def true_lists(triples, mode: str):
+    """{key: sorted true members} — get_true_head_and_tail (dataloader.py:77-85) keyed per mode."""
+    out = {}
+    for h, r, t in np.asarray(triples).tolist():
+        if mode == 'head-batch':
+            out.setdefault((r, t), set()).add(h)
+        else:
+            out.setdefault((h, r), set()).add(t)
+    return {k: np.array(sorted(v), dtype=np.int64) for k, v in out.items()}
+
+
+def subsampling_weights(triples):
+    """sqrt(1 / (count(h,r) + count(t,-r-1))) per triple, counts from 4 (dataloader.py:40-42, :68-75)."""
+    cnt = {}
+    for h, r, t in np.asarray(triples).tolist():
+        cnt[(h, r)] = cnt.get((h, r), 3) + 1
+        cnt[(t, -r - 1)] = cnt.get((t, -r - 1), 3) + 1
+    return np.array([torch.sqrt(1 / torch.Tensor([cnt[(h, r)] + cnt[(t, -r - 1)]])).item()
+                     for h, r, t in np.asarray(triples).tolist()], dtype=np.float32)
+
+
+def sample_negatives(triples, batch, nentity: int, n: int, mode: str, key: int, max_draws: int):
+    """(pos [B,3], neg [B,n], ok [B]) for the device sampler's stream; ok=False where max_draws ran out."""
+    triples = np.asarray(triples, dtype=np.int64)
+    lists = true_lists(triples, mode)
+    B = len(batch)
+    pos = triples[np.asarray(batch)]
+    neg = np.zeros((B, n), dtype=np.int64)
+    ok = np.ones(B, dtype=bool)
+    lanes = np.arange(64, dtype=np.uint64)
+    for i in range(B):
+        h, r, t = pos[i].tolist()
+        tl = lists[(r, t)] if mode == 'head-batch' else lists[(h, r)]
+        with np.errstate(over='ignore'):
+            krow = _mix64_np(np.uint64(key) ^ (np.uint64(i) * np.uint64(0xD1B54A32D192ED03)))
+        got = []
+        d = 0
+        while len(got) < n:
+            if d >= max_draws:
+                ok[i] = False
+                break
+            with np.errstate(over='ignore'):
+                x = _mix64_np(krow + (np.uint64(d) + lanes) * np.uint64(0x9E3779B97F4A7C15))
+            e = _mulhi_small(x, nentity)
+            got.extend(e[~np.isin(e, tl)].tolist())
+            d += 64
+        take = got[:n]
+        neg[i, :len(take)] = take
+    return pos, neg, ok

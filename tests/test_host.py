@@ -38,10 +38,12 @@ REF_FLAGS = [
 
 def test_cli_flags_match_reference():
     args = run.parse_args([])
-    # the reference's flags, plus one extension: --row_partition (multi-GPU
-    # entity-row sharding, partition.py), off by default
-    assert set(vars(args)) == {d for _, d, _ in REF_FLAGS} | {"row_partition"}
-    assert args.row_partition is False and run.parse_args(["--row_partition"]).row_partition is True
+    # the reference's flags, plus two extensions, off by default: --row_partition
+    # (multi-GPU entity-row sharding, partition.py), --device_sampler (sampler.py)
+    ext = ("row_partition", "device_sampler")
+    assert set(vars(args)) == {d for _, d, _ in REF_FLAGS} | set(ext)
+    for e in ext:
+        assert getattr(args, e) is False and getattr(run.parse_args(["--" + e]), e) is True
     for opts, dest, default in REF_FLAGS:
         assert getattr(args, dest) == default, dest
         for o in opts:

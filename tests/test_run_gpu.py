@@ -1,0 +1,65 @@
+"""run.py end to end on the GPU (the reference CLI, run.py:159-342): a tiny
+synthetic dataset in the reference's on-disk format, trained with the device
+sampler, checkpointed, resumed with -init for a test pass, and the saved
+checkpoint/config/.npy files in the reference layout (run.py:93-120)."""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from knowledgegraphembedding_amd import run, synth
+
+pytestmark = pytest.mark.gpu
+
+
+def _dataset(root, E=40, R=3):
+    os.makedirs(root, exist_ok=True)
+    with open(os.path.join(root, "entities.dict"), "w") as f:
+        f.writelines(f"{i}\te{i}\n" for i in range(E))
+    with open(os.path.join(root, "relations.dict"), "w") as f:
+        f.writelines(f"{i}\tr{i}\n" for i in range(R))
+    tr = np.stack([synth.randint(1, (400,), E), synth.randint(2, (400,), R), synth.randint(3, (400,), E)], 1)
+    for name, part in (("train.txt", tr[:300]), ("valid.txt", tr[300:350]), ("test.txt", tr[350:])):
+        with open(os.path.join(root, name), "w") as f:
+            f.writelines(f"e{h}\tr{r}\te{t}\n" for h, r, t in part.tolist())
+
+
+def _metrics(log_file, prefix):
+    """{metric: value} from the reference-format log lines '<prefix><metric> at step <s>: <v>'."""
+    out = {}
+    for line in open(log_file):
+        msg = line.split("INFO", 1)[-1].strip()
+        if msg.startswith(prefix):
+            k, v = msg[len(prefix):].split(" at step ")
+            out[k.strip()] = float(v.split(":")[1])
+    return out
+
+
+def test_run_train_checkpoint_resume(tmp_path):
+    data, save = str(tmp_path / "data"), str(tmp_path / "save")
+    _dataset(data)
+    torch.manual_seed(0)
+    args = run.parse_args(["--cuda", "--do_train", "--do_valid", "--do_test", "--device_sampler", "--data_path", data,
+                           "--model", "RotatE", "-de", "-n", "16", "-b", "32", "-d", "16", "-g", "6.0", "-adv",
+                           "-lr", "0.01", "--max_steps", "30", "--valid_steps", "20", "--log_steps", "10",
+                           "--save_checkpoint_steps", "20", "--test_batch_size", "8", "-save", save, "-cpu", "1"])
+    run.main(args)
+    for f in ("checkpoint", "config.json", "entity_embedding.npy", "relation_embedding.npy"):
+        assert os.path.exists(os.path.join(save, f)), f
+    test1 = _metrics(os.path.join(save, "train.log"), "Test ")
+    assert set(test1) == {"MRR", "MR", "HITS@1", "HITS@3", "HITS@10"}
+    assert 0 < test1["MRR"] <= 1 and test1["MR"] >= 1
+    cfg = json.load(open(os.path.join(save, "config.json")))
+    assert cfg["model"] == "RotatE" and cfg["hidden_dim"] == 16 and cfg["double_entity_embedding"]
+    ckpt = torch.load(os.path.join(save, "checkpoint"), map_location="cpu", weights_only=True)
+    assert ckpt["step"] == 29
+    np.testing.assert_array_equal(np.load(os.path.join(save, "entity_embedding.npy")),
+                                  ckpt["model_state_dict"]["entity_embedding"].numpy())
+    # resume: -init restores the trained model; its test metrics equal the first run's
+    args2 = run.parse_args(["--cuda", "--do_test", "-init", save, "--test_batch_size", "8", "-cpu", "1"])
+    run.main(args2)
+    test2 = _metrics(os.path.join(save, "test.log"), "Test ")
+    for k in test1:
+        assert test2[k] == pytest.approx(test1[k], rel=0, abs=1e-12), k
