@@ -52,6 +52,114 @@ class _TableScore(torch.autograd.Function):
         return ge, gr, (gm.view_as(modulus) if has_mod else None), None, None, None, None, None, None
 
 
+class StepLog(dict):
+    """train_step's log — the reference's {name: float} dict (model.py:305-312)
+    — filled from the device on first read.
+
+    The step's four losses and the device error flag are copied into a pinned
+    host slot behind an event; reading any key (or iterating, printing, json
+    dumping) waits for that event and raises the deferred error if the step
+    saw an out-of-range index.  Until then the host is free to enqueue the
+    next step, so the GPU does not idle while Python prepares it."""
+
+    __slots__ = ('_src',)
+
+    def __init__(self, src):
+        super().__init__()
+        self._src = src  # (host [5] tensor, event, has_regularization, device); None once filled
+
+    def _fill(self):
+        src = self._src
+        if src is None:
+            return self
+        self._src = None
+        host, event, has_reg, dev = src
+        if event is not None:
+            event.synchronize()
+        vals = host.tolist()
+        if vals[4] != 0.0:  # device error flag (out-of-range index), copied by the kernels
+            ops.raise_on_device_error(dev)
+        if has_reg:
+            dict.__setitem__(self, 'regularization', vals[3])
+        dict.__setitem__(self, 'positive_sample_loss', vals[0])
+        dict.__setitem__(self, 'negative_sample_loss', vals[1])
+        dict.__setitem__(self, 'loss', vals[2])
+        return self
+
+    def __getitem__(self, k):
+        return dict.__getitem__(self._fill(), k)
+
+    def __setitem__(self, k, v):
+        dict.__setitem__(self._fill(), k, v)
+
+    def __delitem__(self, k):
+        dict.__delitem__(self._fill(), k)
+
+    def __contains__(self, k):
+        return dict.__contains__(self._fill(), k)
+
+    def __iter__(self):
+        return dict.__iter__(self._fill())
+
+    def __len__(self):
+        return dict.__len__(self._fill())
+
+    def __repr__(self):
+        return dict.__repr__(self._fill())
+
+    def __eq__(self, other):
+        return dict.__eq__(self._fill(), other)
+
+    __hash__ = None
+
+    def get(self, k, default=None):
+        return dict.get(self._fill(), k, default)
+
+    def keys(self):
+        return dict.keys(self._fill())
+
+    def values(self):
+        return dict.values(self._fill())
+
+    def items(self):
+        return dict.items(self._fill())
+
+    def copy(self):
+        return dict(self.items())
+
+    def update(self, *a, **k):
+        dict.update(self._fill(), *a, **k)
+
+    def __reduce__(self):
+        return (dict, (dict(self.items()),))
+
+
+class _LogRing:
+    """Pinned host slots for the per-step loss read-back.  Reusing a slot first
+    completes the log that occupied it, so the host runs at most len(slots)
+    steps ahead of the device and a deferred device error surfaces within
+    that many steps even if no log is read."""
+
+    def __init__(self, dev, depth: int = 2):
+        self.dev = dev
+        cuda = dev.type == 'cuda'  # (CPU only under the gloo tests' stand-in kernels)
+        self.slots = [[torch.empty(5, dtype=torch.float32, pin_memory=cuda), torch.cuda.Event() if cuda else None,
+                       None] for _ in range(depth)]
+        self.k = 0
+
+    def push(self, losses: torch.Tensor, has_reg: bool) -> StepLog:
+        slot = self.slots[self.k]
+        self.k = (self.k + 1) % len(self.slots)
+        if slot[2] is not None:
+            slot[2]._fill()
+        slot[0].copy_(losses, non_blocking=True)
+        if slot[1] is not None:
+            slot[1].record()
+        log = StepLog((slot[0], slot[1], has_reg, self.dev))
+        slot[2] = log
+        return log
+
+
 class KGEModel(nn.Module):
     def __init__(self, model_name, nentity, nrelation, hidden_dim, gamma,
                  double_entity_embedding=False, double_relation_embedding=False):
@@ -89,6 +197,9 @@ class KGEModel(nn.Module):
 
         self._scalars = None
         self._grad_bufs = None
+        # train_step returns a StepLog filled on first read instead of waiting
+        # for the step's losses (False: wait inside train_step, as the reference)
+        self.defer_log = True
         # leave the dense gradients in .grad after a fused train_step, as
         # loss.backward() does in the reference; False skips those writes
         self.keep_grads = True
@@ -237,8 +348,11 @@ class KGEModel(nn.Module):
         '''
         A single train step. Apply back-propation and return the loss
         (model.py:252-312).  One fused HIP pass replaces the two forward
-        calls, the loss and loss.backward(); one 4-float D2H copy replaces
-        the three .item() syncs.
+        calls, the loss and loss.backward(); one 5-float D2H copy replaces
+        the three .item() syncs, and nothing waits for it: the returned log
+        (StepLog) is filled on first read, so the host enqueues the next
+        step while this one runs (at most two steps ahead; model.defer_log =
+        False restores the reference's read-back inside the step).
         '''
         model.train()
         optimizer.zero_grad()
@@ -266,15 +380,14 @@ class KGEModel(nn.Module):
         if part is not None:
             part.gather()  # owners' updated rows → every replica
 
-        vals = losses.cpu().tolist()  # the step's only device→host sync
-        if vals[4] != 0.0:  # device error flag (out-of-range index), copied by the kernels
-            ops.raise_on_device_error(dev)
-        log = {}
-        if args.regularization != 0.0:
-            log['regularization'] = vals[3]
-        log['positive_sample_loss'] = vals[0]
-        log['negative_sample_loss'] = vals[1]
-        log['loss'] = vals[2]
+        # the step's only device→host transfer: 4 losses + the error flag into
+        # a pinned slot; the log reads it on first access (StepLog)
+        ring = model.__dict__.get('_log_ring')
+        if ring is None or ring.dev != dev:
+            ring = model.__dict__['_log_ring'] = _LogRing(dev)
+        log = ring.push(losses, args.regularization != 0.0)
+        if not model.defer_log:
+            log._fill()
         return log
 
     # ------------------------------------------------------------- evaluation

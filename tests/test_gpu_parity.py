@@ -259,6 +259,41 @@ def test_index_error():
         ops.raise_on_device_error(DEV)
 
 
+def test_deferred_step_log():
+    """train_step's StepLog: same floats as the synchronous read-back, a bad
+    index raises IndexError when the log is read, or within two further steps
+    when it is never read (the ring bounds the run-ahead)."""
+    import json
+    import pickle
+    E, R, d, B, n = 40, 4, 8, 6, 5
+    pos, neg, w = synth.kge_batch(61, B, n, E, R)
+    batch = (torch.from_numpy(pos).to(DEV), torch.from_numpy(neg).to(DEV), torch.from_numpy(w).to(DEV), "tail-batch")
+    args = Namespace(negative_adversarial_sampling=True, adversarial_temperature=1.0, uni_weight=False,
+                     regularization=1e-3, dp_group=None)
+    logs = {}
+    for defer in (True, False):
+        m, *_ = build_model("DistMult", E, R, d, 12.0, 5)
+        m.defer_log = defer
+        opt = KGEAdam([p for p in m.parameters() if p.requires_grad], lr=1e-3)
+        logs[defer] = [KGEModel.train_step(m, opt, iter([batch]), args) for _ in range(3)]
+    for a, b in zip(logs[True], logs[False]):
+        assert dict(a.items()) == dict(b.items())
+        assert set(a) == {"regularization", "positive_sample_loss", "negative_sample_loss", "loss"}
+        assert json.loads(json.dumps(a)) == b and pickle.loads(pickle.dumps(a)) == b
+    bad_neg = neg.copy()
+    bad_neg[2, 3] = E + 7
+    bad = (batch[0], torch.from_numpy(bad_neg).to(DEV), batch[2], "tail-batch")
+    m, *_ = build_model("DistMult", E, R, d, 12.0, 5)
+    opt = KGEAdam([p for p in m.parameters() if p.requires_grad], lr=1e-3)
+    log = KGEModel.train_step(m, opt, iter([bad]), args)
+    with pytest.raises(IndexError):
+        log["loss"]
+    KGEModel.train_step(m, opt, iter([bad]), args)  # unread
+    with pytest.raises(IndexError):
+        for _ in range(2):
+            KGEModel.train_step(m, opt, iter([batch]), args)
+
+
 # ------------------------------------------------------------------ Adam
 def test_kge_adam_matches_torch_adam():
     torch.manual_seed(0)
