@@ -50,6 +50,7 @@ WORKLOADS = {
                              name="RotatE YAGO3-10-shape train_step, entity rows partitioned over the ranks "
                                   "(reduce-scatter grads to owners, shard Adam, all-gather rows)"),
 }
+TIMER_PERIOD = 8
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
 
 
@@ -129,9 +130,12 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
+    ap.add_argument("--no-stage-timer", action="store_true",
+                    help="skip the per-stage HIP events (roofline then comes from the committed rocprof summary)")
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="fb15k")
     ap.add_argument("--traffic-json", default=None,
-                    help="rocprofv3 PMC summary (tools/pmc_traffic.py output) for roofline.traffic")
+                    help="rocprofv3 PMC summary (tools/pmc_traffic.py output) for roofline.traffic "
+                         "(default: the committed profiles/pmc_traffic.json of this workload)")
     a = ap.parse_args()
     global E, R, D, B, NNEG
     wl = WORKLOADS[a.workload]
@@ -189,7 +193,8 @@ def main():
     torch.cuda.synchronize()
 
     lib = _lib.load()
-    _lib.check(lib.kge_stage_timer(1, None, 0), "kge_stage_timer")
+    # per-stage HIP events on one step in TIMER_PERIOD (every step's events cost ~4 %)
+    _lib.check(lib.kge_stage_timer(0 if a.no_stage_timer else 1, None, TIMER_PERIOD), "kge_stage_timer")
     if group is not None:
         dist.barrier()
     torch.cuda.synchronize()
@@ -212,10 +217,11 @@ def main():
     calls = max(1.0, float(stage[6]))
     row_ms = float(stage[1]) / calls
     row_bytes = algorithmic_row_bytes(B, NNEG, 2 * D, D)
-    achieved = row_bytes / (row_ms * 1e-3) / 1e9
+    achieved = row_bytes / (row_ms * 1e-3) / 1e9 if row_ms > 0 else None
     traffic = None
-    if a.traffic_json and os.path.exists(a.traffic_json):
-        with open(a.traffic_json) as f:
+    tj = a.traffic_json or os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "pmc_traffic.json")
+    if a.workload == "fb15k" and os.path.exists(tj):
+        with open(tj) as f:
             traffic = json.load(f).get("hbm_bytes_per_launch")
 
     value = a.steps * B * (NNEG + 1) * world / dt
@@ -238,12 +244,13 @@ def main():
                    "entities": E, "relations": R, "hidden_dim": D, "batch_per_gpu": B, "global_batch": B * world,
                    "negatives": NNEG, "adversarial_temperature": TEMP, "gamma": GAMMA,
                    "parallelism": (f"rowpart{world}" if part is not None else f"dp{world}")},
+        "stage_timed_steps": int(stage[6]),
         "stage_ms": {"build_q": float(stage[0]) / calls, "row_pass": row_ms, "row_epilogue": float(stage[2]) / calls,
                      "csr_join": float(stage[3]) / calls, "entity_pass": float(stage[4]) / calls,
                      "relation_join_finalize": float(stage[5]) / calls,
                      "other_incl_adam_ms": dt / a.steps * 1e3 - float(stage[:6].sum()) / calls},
         "roofline": {"bound": "hbm", "kernel": "k_row (fused negative scoring + self-adversarial loss)",
-                     "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                     "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS if achieved else None,
                      "traffic": traffic, "algorithmic_bytes_per_launch": row_bytes,
                      "avg_launch_ms": row_ms},
     }

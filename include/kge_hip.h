@@ -219,7 +219,10 @@ int kge_rank_filtered(const kge_model_desc *m, int32_t mode, const int64_t *quer
  * 3 wait for the occurrence CSR (built on an internal side stream in parallel
  * with stages 0-2), 4 entity-major gradient pass (+ fused Adam), 5 wait for the
  * relation pass (side stream, parallel with 4) + loss finalisation.
- *   command 1: enable and reset; 0: disable and reset;
+ *   command 1: enable and reset, timing one call in every n_out (n_out <= 0:
+ *              every call) — sampling keeps the event records' own cost
+ *              (~4 % of a step when every call is timed) out of the throughput;
+ *   command 0: disable and reset;
  *   command 2: synchronise the recorded events and write the summed
  *              milliseconds per stage to stage_ms_out[0..5] and the number of
  *              timed calls to stage_ms_out[6] (n_out >= 7).

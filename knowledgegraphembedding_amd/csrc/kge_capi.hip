@@ -135,6 +135,8 @@ hipStream_t as_stream(void* s) { return (hipStream_t)s; }
 // ---- stage timer (bench instrumentation; see kge_stage_timer in the header)
 struct StageTimer {
   bool on = false;
+  int period = 1;              // time one train call in `period`
+  size_t seen = 0;             // train calls since enabled
   std::vector<hipEvent_t> ev;  // (KGE_TIMER_STAGES + 1) events per timed call
   size_t used = 0;             // events recorded so far
   hipEvent_t next(hipStream_t) {
@@ -162,7 +164,25 @@ struct Side {
   hipStream_t s = nullptr;
   hipEvent_t fork = nullptr, csr_done = nullptr, epi_done = nullptr, rel_done = nullptr;
 };
+int env_int(const char* name, int dflt) {
+  const char* e = getenv(name);
+  return e ? atoi(e) : dflt;
+}
+
+// Launch-schedule variants (measured in DESIGN.md; defaults are the fastest):
+//   KGE_SIDE_STREAM=0  everything on the caller's stream (no cross-stream events)
+//   KGE_REL_MAIN=1     relation pass on the caller's stream after the entity pass
+//   KGE_CSR_JOIN=1     join the CSR before the epilogue instead of before the entity pass
+struct Schedule {
+  int side, rel_main, csr_join_early;
+};
+const Schedule& schedule() {
+  static const Schedule sch = {env_int("KGE_SIDE_STREAM", 1), env_int("KGE_REL_MAIN", 0), env_int("KGE_CSR_JOIN", 0)};
+  return sch;
+}
+
 Side* side_for_device() {
+  if (!schedule().side) return nullptr;
   static Side sides[64];
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
@@ -202,7 +222,7 @@ int run_grad(const kge_model_desc* m, const Geom& geo, int mode, const int64_t* 
   const int Le = m->entity_dim, Lr = m->relation_dim;
   const size_t lds = sizeof(float) * (2 * 64 * (size_t)geo.ns * geo.vec + 2 * (size_t)Le + (size_t)ra.n_lds + 32);
   if (lds > 64 * 1024) return KGE_ERR_DIM;
-  const bool timed = g_timer.on && ra.op == ROW_TRAIN;
+  const bool timed = g_timer.on && ra.op == ROW_TRAIN && (g_timer.seen++ % (size_t)g_timer.period) == 0;
   ra.timer_mid = timed ? &timer_mark : nullptr;
   Side* sd = side_for_device();
   hipStream_t ss = sd ? sd->s : s;
@@ -229,6 +249,8 @@ int run_grad(const kge_model_desc* m, const Geom& geo, int mode, const int64_t* 
   if (st) return st;
   if (sd) hipEventRecord(sd->csr_done, ss);
 
+  const Schedule& sch = schedule();
+  if (sd && sch.csr_join_early) hipStreamWaitEvent(s, sd->csr_done, 0);
   // epilogue (positive score, chain rule)
   st = launch_status(op.row(mode, geo.vec, geo.ns, 1, ra, lds, s));
   if (st) return st;
@@ -242,16 +264,15 @@ int run_grad(const kge_model_desc* m, const Geom& geo, int mode, const int64_t* 
   rl.write_grad = write_grad;
   rl.adam = adam_t(adam ? &adam->relation : nullptr);
   rl.adamk = ak;
-  if (sd) {
+  const bool rel_side = sd && !sch.rel_main;
+  if (rel_side) {
     hipEventRecord(sd->epi_done, s);
     hipStreamWaitEvent(ss, sd->epi_done, 0);
-  }
-  st = launch_status(launch_rel_rows(rl, ss));
-  if (st) return st;
-  if (sd) {
+    st = launch_status(launch_rel_rows(rl, ss));
+    if (st) return st;
     hipEventRecord(sd->rel_done, ss);
-    hipStreamWaitEvent(s, sd->csr_done, 0);  // join 1: the entity pass reads the CSR
   }
+  if (sd && !sch.csr_join_early) hipStreamWaitEvent(s, sd->csr_done, 0);  // join 1: the entity pass reads the CSR
   if (timed) g_timer.mark(s);
 
   EntArgs ea;
@@ -272,7 +293,12 @@ int run_grad(const kge_model_desc* m, const Geom& geo, int mode, const int64_t* 
   if (st) return st;
   if (timed) g_timer.mark(s);
 
-  if (sd) hipStreamWaitEvent(s, sd->rel_done, 0);  // join 2: everything the side stream wrote
+  if (rel_side) {
+    hipStreamWaitEvent(s, sd->rel_done, 0);  // join 2: everything the side stream wrote
+  } else {
+    st = launch_status(launch_rel_rows(rl, s));
+    if (st) return st;
+  }
   fa.row_stats = w.row_stats;
   fa.reg_partial = (reg != 0.f) ? w.reg_partial : nullptr;
   fa.nreg = m->nentity + m->nrelation;
@@ -571,6 +597,8 @@ int kge_stage_timer(int32_t command, float* stage_ms_out, int32_t n_out) {
   if (command == 0 || command == 1) {
     g_timer.on = (command == 1);
     g_timer.used = 0;
+    g_timer.seen = 0;
+    g_timer.period = (command == 1 && n_out > 0) ? n_out : 1;
     return KGE_OK;
   }
   if (command != 2 || !stage_ms_out || n_out < NS_) return KGE_ERR_ARG;

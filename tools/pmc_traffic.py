@@ -18,6 +18,7 @@ import csv
 import glob
 import json
 import os
+import re
 from collections import defaultdict
 
 
@@ -47,7 +48,8 @@ def main():
         wk = sum(w) / len(w) if w else 0.0
         summary[name] = {"launches": max(len(f), len(w)), "fetch_kib_raw": fk, "write_kib": wk,
                          "hbm_bytes_per_launch": (2.0 * fk + wk) * 1024.0}
-    sel = {k: v for k, v in summary.items() if a.kernel in k}
+    # exact kernel name (template arguments aside): "k_row" must not pick up "k_row_epi"
+    sel = {k: v for k, v in summary.items() if re.search(r"(^|[:\s])" + re.escape(a.kernel) + r"[<(]", k)}
     tot_l = sum(v["launches"] for v in sel.values())
     main_bytes = (sum(v["hbm_bytes_per_launch"] * v["launches"] for v in sel.values()) / tot_l) if tot_l else None
     out = {"kernel": a.kernel, "hbm_bytes_per_launch": main_bytes,

@@ -16,4 +16,8 @@ if [ "${PMC:-1}" = "1" ]; then
     rc=$?; echo "pmc $C rc=$rc"; [ $rc -ne 0 ] && { tail -20 "$OUT/pmc_$C.err"; exit $rc; }
   done
 fi
+if [ "${PMC:-1}" = "1" ]; then
+  python3 "$ROOT/tools/pmc_traffic.py" "$OUT" --kernel k_row -o "$OUT/pmc_traffic.json" > /dev/null &&
+  python3 "$ROOT/tools/pmc_traffic.py" "$OUT" --kernel k_entity -o "$OUT/pmc_traffic_entity.json" > /dev/null
+fi
 find "$OUT" -name "*.csv" | head -20
