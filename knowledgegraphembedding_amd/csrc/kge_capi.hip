@@ -119,7 +119,7 @@ GradWs carve_grad(void* ws, const kge_model_desc* m, int64_t B, int64_t n, size_
   w.ent_contrib = c.take<float>(2 * B * (int64_t)m->entity_dim);
   w.rel_contrib = c.take<float>(B * (int64_t)m->relation_dim);
   w.row_stats = c.take<float>(B * 4);
-  w.reg_partial = c.take<float>(nb);
+  w.reg_partial = c.take<float>(8 * m->nentity + m->nrelation);  // per (entity, column slice) + per relation
   w.wsum = c.take<float>(4);
   w.keys = c.take<int32_t>(N);
   w.cnt = c.take<int32_t>(nb);
@@ -260,7 +260,25 @@ int run_grad(const kge_model_desc* m, const Geom& geo, int mode, const int64_t* 
   RelArgs rl;
   rl.rel = m->relation_embedding; rl.R = m->nrelation; rl.E = m->nentity; rl.B = B; rl.Bn = B * n; rl.Lr = Lr;
   rl.off = w.off; rl.occ = w.occ; rl.rel_contrib = w.rel_contrib; rl.reg3 = 3.f * reg;
-  rl.reg_partial = w.reg_partial + m->nentity; rl.grad_rel = grad_relation;
+  // entity pass variant: column slices (k_entity_sl) when the row fits one
+  // 16-B slot per lane per slice; KGE_ENT_SLICES=0 selects the row-per-wave pass
+  int nsl = 0;
+  {
+    static const int forced = env_int("KGE_ENT_SLICES", -1);
+    const int S = geo.eg.S;
+    auto fits = [&](int k) { return (S + k - 1) / k <= 64; };
+    if (geo.vec == 4 && forced != 0) {
+      int k = forced;
+      if (k < 0) {  // smallest power of two that fits and keeps the q column slice ≤ 2 MiB (half an XCD L2)
+        const double qslice = (double)B * Le * sizeof(float);
+        k = 1;
+        while (k < 8 && (!fits(k) || qslice / k > 2.0 * 1024 * 1024)) k *= 2;
+      }
+      if ((k == 1 || k == 2 || k == 4 || k == 8) && fits(k)) nsl = k;
+    }
+  }
+  const int64_t ent_parts = m->nentity * (int64_t)(nsl > 0 ? nsl : 1);
+  rl.reg_partial = w.reg_partial + ent_parts; rl.grad_rel = grad_relation;
   rl.write_grad = write_grad;
   rl.adam = adam_t(adam ? &adam->relation : nullptr);
   rl.adamk = ak;
@@ -287,6 +305,12 @@ int run_grad(const kge_model_desc* m, const Geom& geo, int mode, const int64_t* 
     return e ? atoi(e) : 3;  // measured: 4 waves/SIMD spills and runs slower
   }();
   ea.minw = ent_minw;
+  ea.nsl = nsl;
+  if (nsl > 0) {
+    static const int pf = env_int("KGE_ENT_PF", 4);
+    ea.minw = pf;
+  }
+  ea.slice_w = nsl > 0 ? (geo.eg.S + nsl - 1) / nsl : 0;
   ea.adam = adam_t(adam ? &adam->entity : nullptr);
   ea.adamk = ak;
   st = launch_status(op.entity(mode, geo.vec, geo.ns, ea, s));
@@ -301,7 +325,7 @@ int run_grad(const kge_model_desc* m, const Geom& geo, int mode, const int64_t* 
   }
   fa.row_stats = w.row_stats;
   fa.reg_partial = (reg != 0.f) ? w.reg_partial : nullptr;
-  fa.nreg = m->nentity + m->nrelation;
+  fa.nreg = ent_parts + m->nrelation;
   fa.regularization = reg;
   fa.grad_modulus = grad_modulus;
   fa.adam = adam_t((adam && m->model == KGE_PROTATE) ? &adam->modulus : nullptr);

@@ -78,7 +78,10 @@ struct EntArgs {
   float* reg_partial;   // [E] Σ|x|^3 per row (when reg3 != 0)
   float* grad_ent;
   int write_grad;       // store grad_ent (unless the fused optimizer asks not to)
-  int minw;             // k_entity variant: min waves/SIMD the register budget targets (3 or 4)
+  int minw;             // k_entity: min waves/SIMD the register budget targets (3 or 4);
+                        // k_entity_sl: q rows in flight per wave (4 or 8)
+  int nsl;              // > 0: column-sliced pass k_entity_sl with nsl slices of slice_w slots (VEC = 4)
+  int slice_w;
   AdamT adam;           // fused optimizer step (adam.p == null: none)
   AdamK adamk;
 };
