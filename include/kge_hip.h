@@ -140,6 +140,26 @@ int kge_train_step_grads(const kge_model_desc *m, int32_t mode, const int64_t *p
                          float *losses_out, void *workspace, size_t workspace_bytes,
                          int32_t *err_flag, void *stream);
 
+/* Phases of kge_train_step_grads, for callers that overlap the entity-gradient
+ * reduction with the entity pass (data parallel, distributed.py): ROWS runs
+ * the q build, the fused scoring/loss row pass, the epilogue, the occurrence
+ * CSR and the relation pass; ENTITY runs the entity-major pass over rows
+ * [entity_begin, entity_end) only (call it once per chunk, in any order, until
+ * every row is covered); FINALIZE joins the relation pass and writes the
+ * losses (and the pRotatE modulus gradient).  Same stream, same workspace,
+ * same arguments in every phase; ALL = one kge_train_step_grads call. */
+#define KGE_PHASE_ROWS 1
+#define KGE_PHASE_ENTITY 2
+#define KGE_PHASE_FINALIZE 4
+#define KGE_PHASE_ALL 7
+int kge_train_step_grads_phased(const kge_model_desc *m, int32_t mode, const int64_t *pos, const int64_t *neg,
+                                int64_t batch, int64_t nneg, const float *subsampling_weight,
+                                const float *weight_sum, int32_t uni_weight, int64_t uni_batch,
+                                int32_t adversarial, float adversarial_temperature, float regularization,
+                                float *grad_entity, float *grad_relation, float *grad_modulus, float *losses_out,
+                                void *workspace, size_t workspace_bytes, int32_t *err_flag, void *stream,
+                                int32_t phases, int64_t entity_begin, int64_t entity_end);
+
 /*
  * kge_train_step_grads + the optimizer step, fused — replaces model.py:268-303
  * (forward, loss, loss.backward() AND optimizer.step()) for a torch.optim.Adam

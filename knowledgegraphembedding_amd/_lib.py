@@ -17,6 +17,7 @@ MODEL_IDS = {"TransE": 0, "DistMult": 1, "ComplEx": 2, "RotatE": 3, "pRotatE": 4
 MODE_IDS = {"single": 0, "head-batch": 1, "tail-batch": 2}
 DEVERR_INDEX = 1
 DEVERR_SAMPLER = 2
+PHASE_ROWS, PHASE_ENTITY, PHASE_FINALIZE, PHASE_ALL = 1, 2, 4, 7
 ERR_HIP_BASE = 1000
 
 
@@ -73,6 +74,11 @@ SIGNATURES = {
     "kge_train_step_grads": (
         C.c_int,
         [_DESC, _I32, _P, _P, _I64, _I64, _P, _P, _I32, _I64, _I32, _F, _F, _P, _P, _P, _P, _P, _SZ, _P, _P],
+    ),
+    "kge_train_step_grads_phased": (
+        C.c_int,
+        [_DESC, _I32, _P, _P, _I64, _I64, _P, _P, _I32, _I64, _I32, _F, _F, _P, _P, _P, _P, _P, _SZ, _P, _P,
+         _I32, _I64, _I64],
     ),
     "kge_train_step": (
         C.c_int,

@@ -202,7 +202,7 @@ Side* side_for_device() {
 int run_grad(const kge_model_desc* m, const Geom& geo, int mode, const int64_t* pos, const int64_t* neg,
              int64_t neg_stride, int64_t B, int64_t n, RowArgs ra, GradWs w, float* grad_entity,
              float* grad_relation, float* grad_modulus, float reg, FinArgs fa, const kge_adam_desc* adam,
-             int32_t* err, hipStream_t s) {
+             int32_t* err, hipStream_t s, int phases = KGE_PHASE_ALL, int64_t e_begin = 0, int64_t e_end = -1) {
   const ModelOps& op = ops_for(m->model);
   AdamK ak;
   ak.b1 = adam ? adam->beta1 : 0.f;
@@ -222,12 +222,46 @@ int run_grad(const kge_model_desc* m, const Geom& geo, int mode, const int64_t* 
   const int Le = m->entity_dim, Lr = m->relation_dim;
   const size_t lds = sizeof(float) * (2 * 64 * (size_t)geo.ns * geo.vec + 2 * (size_t)Le + (size_t)ra.n_lds + 32);
   if (lds > 64 * 1024) return KGE_ERR_DIM;
-  const bool timed = g_timer.on && ra.op == ROW_TRAIN && (g_timer.seen++ % (size_t)g_timer.period) == 0;
+  const bool all = (phases == KGE_PHASE_ALL);
+  if (e_end < 0) e_end = m->nentity;
+  const bool timed = all && g_timer.on && ra.op == ROW_TRAIN && (g_timer.seen++ % (size_t)g_timer.period) == 0;
   ra.timer_mid = timed ? &timer_mark : nullptr;
   Side* sd = side_for_device();
   hipStream_t ss = sd ? sd->s : s;
   int st;
 
+  const Schedule& sch = schedule();
+  // relation pass beside the entity pass; in phased calls always on the side
+  // stream (or, with no side stream, right after the epilogue)
+  const bool rel_side = sd && (!sch.rel_main || !all);
+
+  // entity pass variant: column slices (k_entity_sl) when the row fits one
+  // 16-B slot per lane per slice; KGE_ENT_SLICES=0 selects the row-per-wave pass
+  int nsl = 0;
+  {
+    static const int forced = env_int("KGE_ENT_SLICES", -1);
+    const int S = geo.eg.S;
+    auto fits = [&](int k) { return (S + k - 1) / k <= 64; };
+    if (geo.vec == 4 && forced != 0) {
+      int k = forced;
+      if (k < 0) {  // smallest power of two that fits and keeps the q column slice ≤ 2 MiB (half an XCD L2)
+        const double qslice = (double)B * Le * sizeof(float);
+        k = 1;
+        while (k < 8 && (!fits(k) || qslice / k > 2.0 * 1024 * 1024)) k *= 2;
+      }
+      if ((k == 1 || k == 2 || k == 4 || k == 8) && fits(k)) nsl = k;
+    }
+  }
+  const int64_t ent_parts = m->nentity * (int64_t)(nsl > 0 ? nsl : 1);
+  RelArgs rl;
+  rl.rel = m->relation_embedding; rl.R = m->nrelation; rl.E = m->nentity; rl.B = B; rl.Bn = B * n; rl.Lr = Lr;
+  rl.off = w.off; rl.occ = w.occ; rl.rel_contrib = w.rel_contrib; rl.reg3 = 3.f * reg;
+  rl.reg_partial = w.reg_partial + ent_parts; rl.grad_rel = grad_relation;
+  rl.write_grad = write_grad;
+  rl.adam = adam_t(adam ? &adam->relation : nullptr);
+  rl.adamk = ak;
+
+  if (phases & KGE_PHASE_ROWS) {
   // fork point: the occurrence CSR needs only the batch indices (recorded
   // before anything else is queued, so the side stream never waits for the
   // row pass)
@@ -249,52 +283,32 @@ int run_grad(const kge_model_desc* m, const Geom& geo, int mode, const int64_t* 
   if (st) return st;
   if (sd) hipEventRecord(sd->csr_done, ss);
 
-  const Schedule& sch = schedule();
-  if (sd && sch.csr_join_early) hipStreamWaitEvent(s, sd->csr_done, 0);
+  if (sd && sch.csr_join_early && all) hipStreamWaitEvent(s, sd->csr_done, 0);
   // epilogue (positive score, chain rule)
   st = launch_status(op.row(mode, geo.vec, geo.ns, 1, ra, lds, s));
   if (st) return st;
   if (timed) g_timer.mark(s);
 
   // relation pass on the side stream once the epilogue's contributions exist
-  RelArgs rl;
-  rl.rel = m->relation_embedding; rl.R = m->nrelation; rl.E = m->nentity; rl.B = B; rl.Bn = B * n; rl.Lr = Lr;
-  rl.off = w.off; rl.occ = w.occ; rl.rel_contrib = w.rel_contrib; rl.reg3 = 3.f * reg;
-  // entity pass variant: column slices (k_entity_sl) when the row fits one
-  // 16-B slot per lane per slice; KGE_ENT_SLICES=0 selects the row-per-wave pass
-  int nsl = 0;
-  {
-    static const int forced = env_int("KGE_ENT_SLICES", -1);
-    const int S = geo.eg.S;
-    auto fits = [&](int k) { return (S + k - 1) / k <= 64; };
-    if (geo.vec == 4 && forced != 0) {
-      int k = forced;
-      if (k < 0) {  // smallest power of two that fits and keeps the q column slice ≤ 2 MiB (half an XCD L2)
-        const double qslice = (double)B * Le * sizeof(float);
-        k = 1;
-        while (k < 8 && (!fits(k) || qslice / k > 2.0 * 1024 * 1024)) k *= 2;
-      }
-      if ((k == 1 || k == 2 || k == 4 || k == 8) && fits(k)) nsl = k;
-    }
-  }
-  const int64_t ent_parts = m->nentity * (int64_t)(nsl > 0 ? nsl : 1);
-  rl.reg_partial = w.reg_partial + ent_parts; rl.grad_rel = grad_relation;
-  rl.write_grad = write_grad;
-  rl.adam = adam_t(adam ? &adam->relation : nullptr);
-  rl.adamk = ak;
-  const bool rel_side = sd && !sch.rel_main;
   if (rel_side) {
     hipEventRecord(sd->epi_done, s);
     hipStreamWaitEvent(ss, sd->epi_done, 0);
     st = launch_status(launch_rel_rows(rl, ss));
     if (st) return st;
     hipEventRecord(sd->rel_done, ss);
+  } else if (!all) {
+    st = launch_status(launch_rel_rows(rl, s));
+    if (st) return st;
   }
-  if (sd && !sch.csr_join_early) hipStreamWaitEvent(s, sd->csr_done, 0);  // join 1: the entity pass reads the CSR
+  }  // KGE_PHASE_ROWS
+
+  if (phases & KGE_PHASE_ENTITY) {
+  if (sd && !(all && sch.csr_join_early)) hipStreamWaitEvent(s, sd->csr_done, 0);  // join 1: the entity pass reads the CSR
   if (timed) g_timer.mark(s);
 
   EntArgs ea;
   ea.ent = m->entity_embedding; ea.modulus = m->modulus; ea.E = m->nentity; ea.Le = Le; ea.eg = geo.eg;
+  ea.e_begin = e_begin; ea.e_end = e_end;
   ea.c = c; ea.off = w.off; ea.occ = w.occ; ea.Bn = B * n; ea.n = n;
   ea.g = (ra.op == ROW_TRAIN) ? w.g : ra.g_in;
   ea.q = w.q; ea.ent_contrib = w.ent_contrib; ea.reg3 = 3.f * reg; ea.reg_partial = w.reg_partial;
@@ -313,13 +327,17 @@ int run_grad(const kge_model_desc* m, const Geom& geo, int mode, const int64_t* 
   ea.slice_w = nsl > 0 ? (geo.eg.S + nsl - 1) / nsl : 0;
   ea.adam = adam_t(adam ? &adam->entity : nullptr);
   ea.adamk = ak;
-  st = launch_status(op.entity(mode, geo.vec, geo.ns, ea, s));
-  if (st) return st;
+  if (e_end > e_begin) {
+    st = launch_status(op.entity(mode, geo.vec, geo.ns, ea, s));
+    if (st) return st;
+  }
   if (timed) g_timer.mark(s);
+  }  // KGE_PHASE_ENTITY
 
+  if (!(phases & KGE_PHASE_FINALIZE)) return KGE_OK;
   if (rel_side) {
     hipStreamWaitEvent(s, sd->rel_done, 0);  // join 2: everything the side stream wrote
-  } else {
+  } else if (all) {
     st = launch_status(launch_rel_rows(rl, s));
     if (st) return st;
   }
@@ -463,7 +481,8 @@ static int train_impl(const kge_model_desc* m, int32_t mode, const int64_t* pos,
                       int64_t nneg, const float* subsampling_weight, const float* weight_sum, int32_t uni_weight,
                       int64_t uni_batch, int32_t adversarial, float adversarial_temperature, float regularization,
                       const kge_adam_desc* adam, float* grad_entity, float* grad_relation, float* grad_modulus,
-                      float* losses_out, void* workspace, size_t workspace_bytes, int32_t* err_flag, void* stream) {
+                      float* losses_out, void* workspace, size_t workspace_bytes, int32_t* err_flag, void* stream,
+                      int32_t phases = KGE_PHASE_ALL, int64_t e_begin = 0, int64_t e_end = -1) {
   Geom geo;
   int st = check_model(m, &geo);
   if (st) return st;
@@ -511,8 +530,24 @@ static int train_impl(const kge_model_desc* m, int32_t mode, const int64_t* pos,
   fa.uni_n = (float)ub;
   fa.losses = losses_out;
   fa.err = err_flag;
+  if (phases < 1 || phases > KGE_PHASE_ALL) return KGE_ERR_ARG;
+  if (e_end < 0) e_end = m->nentity;
+  if (e_begin < 0 || e_begin > e_end || e_end > m->nentity) return KGE_ERR_ARG;
   return run_grad(m, geo, mode, pos, neg, nneg, batch, nneg, ra, w, grad_entity, grad_relation,
-                  m->model == KGE_PROTATE ? grad_modulus : nullptr, regularization, fa, adam, err_flag, s);
+                  m->model == KGE_PROTATE ? grad_modulus : nullptr, regularization, fa, adam, err_flag, s, phases,
+                  e_begin, e_end);
+}
+
+int kge_train_step_grads_phased(const kge_model_desc* m, int32_t mode, const int64_t* pos, const int64_t* neg,
+                                int64_t batch, int64_t nneg, const float* subsampling_weight,
+                                const float* weight_sum, int32_t uni_weight, int64_t uni_batch, int32_t adversarial,
+                                float adversarial_temperature, float regularization, float* grad_entity,
+                                float* grad_relation, float* grad_modulus, float* losses_out, void* workspace,
+                                size_t workspace_bytes, int32_t* err_flag, void* stream, int32_t phases,
+                                int64_t entity_begin, int64_t entity_end) {
+  return train_impl(m, mode, pos, neg, batch, nneg, subsampling_weight, weight_sum, uni_weight, uni_batch, adversarial,
+                    adversarial_temperature, regularization, nullptr, grad_entity, grad_relation, grad_modulus,
+                    losses_out, workspace, workspace_bytes, err_flag, stream, phases, entity_begin, entity_end);
 }
 
 int kge_train_step_grads(const kge_model_desc* m, int32_t mode, const int64_t* pos, const int64_t* neg,

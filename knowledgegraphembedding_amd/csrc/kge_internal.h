@@ -64,6 +64,7 @@ struct EntArgs {
   const float* ent;
   const float* modulus;
   int64_t E;
+  int64_t e_begin, e_end;  // entity rows this launch covers (a chunk of [0, E))
   int Le;
   RowGeom eg;
   Consts c;

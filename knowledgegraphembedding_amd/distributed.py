@@ -9,7 +9,11 @@ normaliser is global: every rank
      or uses 1 / (B * world) under --uni_weight;
   2. runs the fused kernel on its shard → dense partial gradients;
   3. all-reduces (SUM) the entity/relation(/modulus) gradients and the four
-     loss partials in one flat bucket list;
+     loss partials — the entity gradient in row chunks, each chunk's
+     all-reduce issued (async, RCCL's own stream) as soon as the entity pass
+     has queued it, so the reduction of chunk k overlaps the computation of
+     chunk k+1 (bucket entity-row ranges as the entity-major
+     backward finishes them);
   4. steps the (replicated) optimizer identically.
 
 The regularisation term reads the full tables, so only rank 0 adds it before
@@ -18,9 +22,19 @@ the sum (it would otherwise be counted world_size times).
 from __future__ import annotations
 
 import copy
+import os
 
 import torch
 import torch.distributed as dist
+
+DP_CHUNKS = int(os.environ.get("KGE_DP_CHUNKS", "4"))
+
+
+def entity_chunks(nentity: int, chunks: int = DP_CHUNKS):
+    """Contiguous entity-row ranges for the overlapped gradient all-reduce."""
+    chunks = max(1, min(chunks, nentity))
+    step = -(-nentity // chunks)
+    return [(e0, min(nentity, e0 + step)) for e0 in range(0, nentity, step)]
 
 
 def dp_allreduce_(tensors, group=None) -> None:
@@ -47,12 +61,22 @@ def dp_train_grads(model, positive_sample, negative_sample, subsampling_weight, 
     if rank != 0 and args.regularization != 0.0:
         local_args = copy.copy(args)
         local_args.regularization = 0.0
+    pending = []
+
+    def reduce_chunk(e0, e1, grad_entity):
+        pending.append(dist.all_reduce(grad_entity[e0:e1], op=dist.ReduceOp.SUM, group=group, async_op=True))
+
     losses = model.compute_train_grads(positive_sample, negative_sample, subsampling_weight, mode, local_args,
-                                       weight_sum=wsum, uni_batch=B * world)
-    grads = [model.entity_embedding.grad, model.relation_embedding.grad]
+                                       weight_sum=wsum, uni_batch=B * world,
+                                       entity_chunks=entity_chunks(model.entity_embedding.shape[0]),
+                                       on_entity_chunk=reduce_chunk)
+    rest = [model.relation_embedding.grad]
     if model.model_name == 'pRotatE' and model.modulus.grad is not None:
-        grads.append(model.modulus.grad)
-    dp_allreduce_(grads + [losses], group)
+        rest.append(model.modulus.grad)
+    for t in rest + [losses]:
+        pending.append(dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group, async_op=True))
+    for work in pending:
+        work.wait()
     # loss = (pos + neg) / 2 + reg must be recomputed from the summed parts
     losses[2] = (losses[0] + losses[1]) / 2 + losses[3]
     return losses

@@ -22,7 +22,7 @@ import numpy as np
 import torch
 import torch.nn as nn
 
-from . import ops
+from . import _lib, ops
 from .filters import FilterIndex
 
 _MODELS = ['TransE', 'DistMult', 'ComplEx', 'RotatE', 'pRotatE']
@@ -315,12 +315,16 @@ class KGEModel(nn.Module):
         return bufs
 
     def compute_train_grads(self, positive_sample, negative_sample, subsampling_weight, mode, args,
-                            weight_sum=None, uni_batch=0, optimizer=None):
+                            weight_sum=None, uni_batch=0, optimizer=None, entity_chunks=None, on_entity_chunk=None):
         """Fused forward + self-adversarial loss + backward (model.py:268-301).
         Writes dense .grad tensors; returns the device [5] vector
         (positive_sample_loss, negative_sample_loss, loss, regularization, error flag).
         With a KGEAdam `optimizer` the Adam update is applied inside the same
-        gradient passes (the optimizer's next step() then skips these tables)."""
+        gradient passes (the optimizer's next step() then skips these tables).
+        With `entity_chunks` [(e0, e1), ...] the entity-gradient pass runs one
+        row range at a time and `on_entity_chunk(e0, e1, grad_entity)` is called
+        as soon as each range is queued (the data-parallel path starts that
+        range's all-reduce there, overlapping the next range's computation)."""
         dev = ops._require_device(self.entity_embedding)
         g, rng = self._host_scalars()
         ge, gr, gm, losses = self._grad_buffers()
@@ -328,13 +332,24 @@ class KGEModel(nn.Module):
         if optimizer is not None and self.fuse_optimizer and hasattr(optimizer, 'prepare_fused'):
             adam = optimizer.prepare_fused(self.entity_embedding, self.relation_embedding, self._modulus(),
                                            write_grad=self.keep_grads)
-        ops.train_step_grads(
-            self.desc(), mode, positive_sample, negative_sample, subsampling_weight, dev,
-            adversarial=bool(args.negative_adversarial_sampling),
-            temperature=float(getattr(args, 'adversarial_temperature', 1.0)),
-            uni_weight=bool(args.uni_weight), regularization=float(args.regularization),
-            grad_entity=ge, grad_relation=gr, grad_modulus=gm, losses=losses,
-            weight_sum_dev=weight_sum, uni_batch=uni_batch, adam=adam)
+        kw = dict(adversarial=bool(args.negative_adversarial_sampling),
+                  temperature=float(getattr(args, 'adversarial_temperature', 1.0)),
+                  uni_weight=bool(args.uni_weight), regularization=float(args.regularization),
+                  grad_entity=ge, grad_relation=gr, grad_modulus=gm, losses=losses,
+                  weight_sum_dev=weight_sum, uni_batch=uni_batch)
+        desc = self.desc()
+        if entity_chunks is None:
+            ops.train_step_grads(desc, mode, positive_sample, negative_sample, subsampling_weight, dev, adam=adam,
+                                 **kw)
+        else:
+            run = lambda **x: ops.train_step_grads(desc, mode, positive_sample, negative_sample,  # noqa: E731
+                                                   subsampling_weight, dev, **kw, **x)
+            run(phases=_lib.PHASE_ROWS)
+            for e0, e1 in entity_chunks:
+                run(phases=_lib.PHASE_ENTITY, entity_range=(e0, e1))
+                if on_entity_chunk is not None:
+                    on_entity_chunk(e0, e1, ge)
+            run(phases=_lib.PHASE_FINALIZE)
         if self.entity_embedding.requires_grad:
             self.entity_embedding.grad = ge
         if self.relation_embedding.requires_grad:

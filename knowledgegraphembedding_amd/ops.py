@@ -176,9 +176,12 @@ def train_step_grads(desc: _lib.ModelDesc, mode: str, pos: torch.Tensor, neg: to
                      dev, *, adversarial: bool, temperature: float, uni_weight: bool, regularization: float,
                      grad_entity: torch.Tensor, grad_relation: torch.Tensor, grad_modulus: Optional[torch.Tensor],
                      losses: torch.Tensor, weight_sum_dev: Optional[torch.Tensor] = None,
-                     uni_batch: int = 0, adam: Optional[_lib.AdamDesc] = None) -> None:
+                     uni_batch: int = 0, adam: Optional[_lib.AdamDesc] = None, phases: int = _lib.PHASE_ALL,
+                     entity_range: Optional[tuple] = None) -> None:
     """Fused scoring + loss + backward into the given dense grad buffers (model.py:252-301);
-    with `adam`, also the optimizer step, fused into the gradient passes (model.py:303)."""
+    with `adam`, also the optimizer step, fused into the gradient passes (model.py:303).
+    `phases` / `entity_range` run a part of the step (kge_train_step_grads_phased): the
+    data-parallel path reduces entity-row chunks while later chunks are computed."""
     if mode not in ("head-batch", "tail-batch"):
         raise ValueError("Training batch mode %s not supported" % mode)
     pos = _idx(pos, dev)
@@ -196,7 +199,13 @@ def train_step_grads(desc: _lib.ModelDesc, mode: str, pos: torch.Tensor, neg: to
               int(bool(uni_weight)), int(uni_batch), int(bool(adversarial)), float(temperature), float(regularization))
     tail = (grad_entity.data_ptr(), grad_relation.data_ptr(), _ptr(grad_modulus), losses.data_ptr(), ws.data_ptr(),
             ws.numel(), st.err.data_ptr(), _stream(dev))
-    if adam is None:
+    if phases != _lib.PHASE_ALL or entity_range is not None:
+        if adam is not None:
+            raise ValueError("phased train steps take no fused optimizer")
+        e0, e1 = entity_range if entity_range is not None else (0, desc.nentity)
+        _lib.check(lib.kge_train_step_grads_phased(*common, *tail, int(phases), int(e0), int(e1)),
+                   "kge_train_step_grads_phased")
+    elif adam is None:
         _lib.check(lib.kge_train_step_grads(*common, *tail), "kge_train_step_grads")
     else:
         _lib.check(lib.kge_train_step(*common, adam, *tail), "kge_train_step")

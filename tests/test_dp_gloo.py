@@ -40,8 +40,11 @@ def _make_model(name):
     return KGEModel(name, E, R, D, GAMMA, de, dr)
 
 
-def oracle_rank_grads(model, pos, neg, w, mode, args, weight_sum=None, uni_batch=0, optimizer=None):
-    """Per-rank objective: the rank's share of the global loss."""
+def oracle_rank_grads(model, pos, neg, w, mode, args, weight_sum=None, uni_batch=0, optimizer=None,
+                      entity_chunks=None, on_entity_chunk=None):
+    """Per-rank objective: the rank's share of the global loss.  Honours the
+    chunk hook of KGEModel.compute_train_grads (called after the gradient is
+    complete, chunk by chunk, as the kernels would)."""
     name = model.model_name
     ent = model.entity_embedding.detach().clone().requires_grad_(True)
     rel = model.relation_embedding.detach().clone().requires_grad_(True)
@@ -68,6 +71,9 @@ def oracle_rank_grads(model, pos, neg, w, mode, args, weight_sum=None, uni_batch
     model.relation_embedding.grad = rel.grad
     if mod is not None:
         model.modulus.grad = mod.grad
+    for e0, e1 in (entity_chunks or []):
+        if on_entity_chunk is not None:
+            on_entity_chunk(e0, e1, model.entity_embedding.grad)
     return torch.stack([pl.detach(), nl.detach(), loss.detach(), reg.detach(), torch.zeros(())]).float()
 
 
