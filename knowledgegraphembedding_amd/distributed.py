@@ -50,8 +50,10 @@ def dp_weight_sum(subsampling_weight: torch.Tensor, group=None) -> torch.Tensor:
     return ws
 
 
-def dp_train_grads(model, positive_sample, negative_sample, subsampling_weight, mode, args):
-    """Fused per-rank gradients + global reduction; returns the global [4] loss vector."""
+def dp_train_grads(model, positive_sample, negative_sample, subsampling_weight, mode, args, optimizer=None):
+    """Fused per-rank gradients + global reduction; returns the global [5] loss vector.
+    With a KGEAdam `optimizer` the entity table's update runs chunk by chunk as
+    each chunk's all-reduce lands (the next train_step optimizer.step() skips it)."""
     group = args.dp_group
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
@@ -66,16 +68,20 @@ def dp_train_grads(model, positive_sample, negative_sample, subsampling_weight, 
     def reduce_chunk(e0, e1, grad_entity):
         pending.append(dist.all_reduce(grad_entity[e0:e1], op=dist.ReduceOp.SUM, group=group, async_op=True))
 
+    chunks = entity_chunks(model.entity_embedding.shape[0])
     losses = model.compute_train_grads(positive_sample, negative_sample, subsampling_weight, mode, local_args,
-                                       weight_sum=wsum, uni_batch=B * world,
-                                       entity_chunks=entity_chunks(model.entity_embedding.shape[0]),
+                                       weight_sum=wsum, uni_batch=B * world, entity_chunks=chunks,
                                        on_entity_chunk=reduce_chunk)
     rest = [model.relation_embedding.grad]
     if model.model_name == 'pRotatE' and model.modulus.grad is not None:
         rest.append(model.modulus.grad)
     for t in rest + [losses]:
         pending.append(dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group, async_op=True))
-    for work in pending:
+    if optimizer is not None and hasattr(optimizer, 'step_param') and model.entity_embedding.requires_grad:
+        # Adam on each entity-row chunk as soon as its reduction lands, while
+        # the later chunks are still on the wire
+        optimizer.step_param(model.entity_embedding, chunks, before_chunk=lambda k: pending[k].wait())
+    for work in pending:  # (waiting twice on a chunk is a no-op)
         work.wait()
     # loss = (pos + neg) / 2 + reg must be recomputed from the summed parts
     losses[2] = (losses[0] + losses[1]) / 2 + losses[3]

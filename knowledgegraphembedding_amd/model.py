@@ -384,7 +384,8 @@ class KGEModel(nn.Module):
             losses = part.train_grads(model, positive_sample, negative_sample, subsampling_weight, mode, args)
         elif dp is not None:
             from .distributed import dp_train_grads
-            losses = dp_train_grads(model, positive_sample, negative_sample, subsampling_weight, mode, args)
+            losses = dp_train_grads(model, positive_sample, negative_sample, subsampling_weight, mode, args,
+                                    optimizer=optimizer)
         else:
             # a KGEAdam optimizer is stepped inside the gradient passes; any
             # other optimizer sees ordinary dense .grad tensors

@@ -73,6 +73,36 @@ class KGEAdam(torch.optim.Optimizer):
         return desc
 
     @torch.no_grad()
+    def step_param(self, p, chunks=None, before_chunk=None) -> bool:
+        """Apply this step's update to ONE parameter now — row range by row
+        range, calling before_chunk(k) before range k (the data-parallel path
+        waits there for that range's all-reduce) — and skip it in the next
+        step().  Same per-element arithmetic as step()."""
+        group = self._group_of(p)
+        if group is None or p.grad is None or id(p) in self._fused_done:
+            return False
+        beta1, beta2 = group['betas']
+        state, step = self._advance(p, group)
+        row_bytes = p[0].numel() * p.element_size() if p.dim() > 1 else 0
+        if chunks is not None and (p.dim() < 2 or row_bytes % 16 != 0 or not p.grad.is_contiguous()):
+            # row ranges would break kge_adam_step's 16-byte alignment: wait for
+            # every range first, then update the whole tensor at once
+            if before_chunk is not None:
+                for k in range(len(chunks)):
+                    before_chunk(k)
+            chunks, before_chunk = None, None
+        if chunks is None:
+            chunks = [(0, p.shape[0] if p.dim() else 1)]
+        for k, (r0, r1) in enumerate(chunks):
+            if before_chunk is not None:
+                before_chunk(k)
+            sl = (slice(r0, r1),) if p.dim() else ()
+            ops.adam_step(p.data[sl], p.grad[sl], state['exp_avg'][sl], state['exp_avg_sq'][sl], step=step,
+                          lr=group['lr'], beta1=beta1, beta2=beta2, eps=group['eps'])
+        self._fused_done.add(id(p))
+        return True
+
+    @torch.no_grad()
     def step(self, closure=None):
         loss = None
         if closure is not None:

@@ -17,7 +17,7 @@ import torch.distributed as dist
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
-from knowledgegraphembedding_amd import KGEModel, synth  # noqa: E402
+from knowledgegraphembedding_amd import KGEAdam, KGEModel, synth  # noqa: E402
 from knowledgegraphembedding_amd.distributed import dp_train_grads  # noqa: E402
 
 
@@ -49,6 +49,37 @@ def main():
         if rank == 0:
             print(f"[dp world={world}] {name}: losses {losses[:3]} vs {ref[:3]}  "
                   f"max|Δg_ent| {np.abs(ge - re).max():.2e}  {'OK' if good else 'MISMATCH'}", flush=True)
+        # two full train_steps with KGEAdam (entity Adam applied chunk by chunk as
+        # each chunk's all-reduce lands) against one process on the whole batch
+        tables = []
+        for group in (dist.group.WORLD, None):
+            torch.manual_seed(0)
+            m = KGEModel(name, 2000, 30, 100, 12.0, de, dr).to(dev)
+            opt = KGEAdam([p for p in m.parameters() if p.requires_grad], lr=1e-2)
+            args.dp_group = group
+            batches = []
+            for k, mode in enumerate(("tail-batch", "head-batch")):
+                pos, neg, w = synth.kge_batch(20 + k, B, n, 2000, 30)
+                if group is not None:
+                    pos, neg, w = pos[sl], neg[sl], w[sl]
+                batches.append((t(pos), t(neg), t(w), mode))
+            it = iter(batches)
+            for _ in range(2):
+                KGEModel.train_step(m, opt, it, args)
+            tables.append((m.entity_embedding.detach().cpu().numpy(), m.relation_embedding.detach().cpu().numpy()))
+        # fp32 summation order differs (per-rank partial sums + all-reduce); an
+        # element whose gradient nearly cancels (|g| ~ Adam's eps) amplifies
+        # that, so the bar is: ≤ 1e-4 of the elements beyond 1e-5, none beyond 2·lr
+        diff_e = np.abs(tables[0][0] - tables[1][0])
+        diff_r = np.abs(tables[0][1] - tables[1][1])
+        d_e, d_r = diff_e.max(), diff_r.max()
+        frac = max((diff_e > 1e-5).mean(), (diff_r > 1e-5).mean())
+        good = frac <= 1e-4 and max(d_e, d_r) <= 2e-2
+        ok &= bool(good)
+        if rank == 0:
+            print(f"[dp world={world}] {name}: 2 Adam steps, max|Δent| {d_e:.2e} max|Δrel| {d_r:.2e} "
+                  f"frac>1e-5 {frac:.1e}  "
+                  f"{'OK' if good else 'MISMATCH'}", flush=True)
     flag = torch.tensor([0 if ok else 1])
     dist.all_reduce(flag)
     dist.destroy_process_group()
