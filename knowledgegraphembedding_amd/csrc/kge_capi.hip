@@ -635,7 +635,7 @@ int kge_rank_filtered(const kge_model_desc* m, int32_t mode, const int64_t* quer
     return launch_status(launch_rank_mfma(a.q, m->entity_embedding, nq, m->nentity, m->entity_dim, a.true_id,
                                           a.s_true, filt_off, filt_ids, bits, a.gt, a.eq, ranks_out, ties_out,
                                           err_flag, s));
-  st = launch_status(launch_filter_bits(filt_off, filt_ids, nq, m->nentity, bits, err_flag, s));
+  st = launch_status(launch_filter_bits(filt_off, filt_ids, a.true_id, nq, m->nentity, bits, err_flag, s));
   if (st) return st;
   TileArgs ta;
   ta.q = a.q; ta.ent = m->entity_embedding; ta.modulus = m->modulus;

@@ -52,8 +52,8 @@ struct FinArgs {
 int launch_rank_mfma(const float* q, const float* ent, int64_t nq, int64_t E, int K, const int64_t* true_id,
                      float* s_true, const int64_t* filt_off, const int64_t* filt_ids, uint32_t* bits, int32_t* gt,
                      int32_t* eq, int64_t* ranks, int32_t* ties, int32_t* err, hipStream_t s);
-int launch_filter_bits(const int64_t* filt_off, const int64_t* filt_ids, int64_t nq, int64_t E, uint32_t* bits,
-                       int32_t* err, hipStream_t s);
+int launch_filter_bits(const int64_t* filt_off, const int64_t* filt_ids, const int64_t* true_id, int64_t nq,
+                       int64_t E, uint32_t* bits, int32_t* err, hipStream_t s);
 int launch_rank_emit(const int32_t* gt, const int32_t* eq, const int64_t* true_id, int64_t nq, int64_t* ranks,
                      int32_t* ties, hipStream_t s);
 int launch_csr(const CsrArgs& a, hipStream_t s);

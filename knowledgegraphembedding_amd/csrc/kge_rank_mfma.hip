@@ -11,10 +11,16 @@
 // are produced by identical instruction sequences and compare consistently.
 //
 // Tile: 128 queries × 128 candidates per workgroup (4 waves as 2×2, each
-// 64×64 = 2×2 MFMA tiles), K staged through LDS 16 deep, transposed to
-// [k][row] so each lane's A/B operand is one conflict-free ds_read_b32.
-// Epilogue: v_cmp → wave ballot → popcounts per query row, summed in LDS,
-// then one integer atomic per (block, query): exact and order-free.
+// 64×64 = 2×2 MFMA tiles), K staged through LDS 32 deep, transposed to
+// [k][row] (rows padded to 132 floats) so each lane's A/B operand is one
+// ds_read_b32; the next slab's global loads are issued into registers before
+// the current slab's MFMAs, so their latency hides behind the matrix work.
+// Candidates are the MFMA rows and queries the columns, so each lane owns two
+// query columns: the epilogue tests its 32 candidates per query against s_true
+// and a 2-word slice of the query's exclusion bitmap (filtered ids, the true
+// id, ids past E) with plain per-lane integer counts, adds the two lane halves,
+// and issues one LDS and then one global integer atomic per (block, query):
+// exact and order-free.
 #include "kge_common.h"
 
 namespace kge {
@@ -23,7 +29,9 @@ namespace {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
-constexpr int BM = 128, BN = 128, BK = 16;
+constexpr int BM = 128, BN = 128, BK = 32;
+constexpr int LDW = 128 + 4;  // padded LDS row: the transposed float4 stores hit 4 bank groups
+constexpr int F4 = (BM * BK / 4) / 256;  // float4 per thread per operand per slab
 
 struct MfmaArgs {
   const float* q;        // [nq, K]
@@ -38,18 +46,19 @@ struct MfmaArgs {
   int32_t* eq;             // [nq]
 };
 
-// Stage a [rows × BK] slab of row-major [*, K] data into LDS as [BK][128].
-// Thread t loads float4 (row t/4 + 64u, k = (t%4)*4 .. +3).
-__device__ __forceinline__ void stage(float (*dst)[128], const float* __restrict__ src, const int64_t* rows,
-                                      int K, int k0, int t) {
+// One [128 rows × BK] slab of row-major [*, K] data: thread t holds float4
+// f = t + 256u (row f / (BK/4), k = (f % (BK/4))·4 .. +3) in registers
+// (fetch), then writes it transposed into LDS as [k][row] (put).
+__device__ __forceinline__ void fetch(float4 (&r)[F4], const float* __restrict__ src, const int64_t* rows, int K,
+                                      int k0, int t) {
 #pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    const int r = (t >> 2) + 64 * u;
-    const int kq = (t & 3) * 4;
-    const int64_t row = rows[r];
+  for (int u = 0; u < F4; ++u) {
+    const int f = t + 256 * u;
+    const int row = f / (BK / 4), kq = (f % (BK / 4)) * 4;
+    const int64_t gr = rows[row];
     float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (row >= 0) {
-      const float* p = src + row * (int64_t)K + k0 + kq;
+    if (gr >= 0) {
+      const float* p = src + gr * (int64_t)K + k0 + kq;
       if (k0 + kq + 3 < K) {
         v = *reinterpret_cast<const float4*>(p);
       } else {
@@ -58,18 +67,26 @@ __device__ __forceinline__ void stage(float (*dst)[128], const float* __restrict
         if (k0 + kq + 2 < K) v.z = p[2];
       }
     }
-    dst[kq + 0][r] = v.x;
-    dst[kq + 1][r] = v.y;
-    dst[kq + 2][r] = v.z;
-    dst[kq + 3][r] = v.w;
+    r[u] = v;
+  }
+}
+__device__ __forceinline__ void put(float (*dst)[LDW], const float4 (&r)[F4], int t) {
+#pragma unroll
+  for (int u = 0; u < F4; ++u) {
+    const int f = t + 256 * u;
+    const int row = f / (BK / 4), kq = (f % (BK / 4)) * 4;
+    dst[kq + 0][row] = r[u].x;
+    dst[kq + 1][row] = r[u].y;
+    dst[kq + 2][row] = r[u].z;
+    dst[kq + 3][row] = r[u].w;
   }
 }
 
 template <bool GATHER>
-__global__ __launch_bounds__(256) void k_rank_mfma(MfmaArgs a) {
-  __shared__ __attribute__((aligned(16))) float As[BK][128];
-  __shared__ __attribute__((aligned(16))) float Bs[BK][128];
-  __shared__ int64_t arow[128], brow[128], tids[128];
+__global__ __launch_bounds__(256, 3) void k_rank_mfma(MfmaArgs a) {
+  __shared__ __attribute__((aligned(16))) float As[BK][LDW];
+  __shared__ __attribute__((aligned(16))) float Bs[BK][LDW];
+  __shared__ int64_t arow[128], brow[128];
   __shared__ float sts[128];
   __shared__ int32_t cgt[128], ceq[128];
   const int t = threadIdx.x, lane = t & 63, w = wave_id();
@@ -80,7 +97,6 @@ __global__ __launch_bounds__(256) void k_rank_mfma(MfmaArgs a) {
     const int64_t q = q0 + t;
     arow[t] = (q < a.nq) ? q : -1;
     const int64_t tid_ = (q < a.nq) ? a.true_id[q] : -1;
-    tids[t] = tid_;
     if (GATHER) {
       brow[t] = (tid_ >= 0 && tid_ < a.E) ? tid_ : -1;
     } else {
@@ -102,70 +118,88 @@ __global__ __launch_bounds__(256) void k_rank_mfma(MfmaArgs a) {
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
   const int kh = lane >> 5, li = lane & 31;
+  float4 ra[F4], rb[F4];
+  fetch(ra, a.q, arow, a.K, 0, t);
+  fetch(rb, a.ent, brow, a.K, 0, t);
   for (int k0 = 0; k0 < a.K; k0 += BK) {
-    stage(As, a.q, arow, a.K, k0, t);
-    stage(Bs, a.ent, brow, a.K, k0, t);
+    put(As, ra, t);
+    put(Bs, rb, t);
     __syncthreads();
+    if (k0 + BK < a.K) {  // next slab's global loads in flight behind the MFMAs
+      fetch(ra, a.q, arow, a.K, k0 + BK, t);
+      fetch(rb, a.ent, brow, a.K, k0 + BK, t);
+    }
 #pragma unroll
     for (int kk = 0; kk < BK / 2; ++kk) {
       // k order: (k0 + 2kk) in lanes 0-31, (k0 + 2kk + 1) in lanes 32-63 —
-      // ascending k across the loop, the same in both passes
-      float af[2], bf[2];
+      // ascending k across the loop, the same in both passes.  Candidates are
+      // the MFMA rows (A), queries the columns (B): a lane's accumulator
+      // column is one query, so the epilogue counts without cross-lane work.
+      float ef[2], qf[2];
 #pragma unroll
-      for (int i = 0; i < 2; ++i) af[i] = As[2 * kk + kh][wm * 64 + i * 32 + li];
+      for (int i = 0; i < 2; ++i) ef[i] = Bs[2 * kk + kh][wm * 64 + i * 32 + li];
 #pragma unroll
-      for (int j = 0; j < 2; ++j) bf[j] = Bs[2 * kk + kh][wn * 64 + j * 32 + li];
+      for (int j = 0; j < 2; ++j) qf[j] = As[2 * kk + kh][wn * 64 + j * 32 + li];
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i], bf[j], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(ef[i], qf[j], acc[i][j], 0, 0, 0);
     }
     __syncthreads();
   }
 
-  // C/D layout: col = lane & 31, row = (reg & 3) + 8 * (reg >> 2) + 4 * (lane >> 5)
+  // C/D layout: col (query) = lane & 31, row (candidate) = (reg & 3) + 8·(reg >> 2) + 4·(lane >> 5)
   if (GATHER) {
-    if (wm != wn) return;
+    // diagonal: candidate row m == query column n; for column li that is
+    // register r = 4·(li >> 3) + (li & 3) of the lane half kh = (li >> 2) & 1
+    if (wm != wn || kh != ((li >> 2) & 1)) return;
+    const int rd = 4 * (li >> 3) + (li & 3);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int n = wn * 64 + i * 32 + li;
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        if (r == rd && arow[n] >= 0) a.s_true[q0 + n] = acc[i][i][r];
+    }
+    return;
+  }
+  const int64_t wbase = e0 >> 5;  // the tile's 128 candidates = bitmap words wbase .. wbase+3
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int n = wn * 64 + j * 32 + li;
+    const int64_t q = arow[n];
+    const float st = sts[n];
+    // excluded candidates of this query among rows wm·64 .. +63: filtered ids
+    // and the true id (bitmap), and ids past E
+    uint32_t ex[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int64_t widx = wbase + wm * 2 + i;
+      const int64_t cbase = e0 + wm * 64 + i * 32;
+      uint32_t word = (q >= 0 && widx < a.W) ? a.fbits[q * a.W + widx] : ~0u;
+      const int64_t valid = a.E - cbase;
+      if (valid < 32) word |= (valid <= 0) ? ~0u : (~0u << valid);
+      ex[i] = word;
+    }
+    int g = 0, e_ = 0;
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int m = wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * kh;
-        const int n = wn * 64 + i * 32 + li;  // diagonal sub-tile j == i
-        if (m == n && arow[m] >= 0) a.s_true[q0 + m] = acc[i][i][r];
+        const int mloc = (r & 3) + 8 * (r >> 2) + 4 * kh;
+        const bool ok = ((ex[i] >> mloc) & 1u) == 0u;
+        const float sc = acc[i][j][r];
+        g += (ok && sc > st) ? 1 : 0;
+        e_ += (ok && sc == st) ? 1 : 0;
       }
-    return;
-  }
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int n = wn * 64 + j * 32 + li;
-      const int64_t e = brow[n];
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int m = wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * kh;
-        const int64_t q = arow[m];
-        bool ok = (q >= 0) && (e >= 0) && (e != tids[m]);
-        if (ok) {
-          const uint32_t word = a.fbits[q * a.W + (e >> 5)];
-          ok = ((word >> (e & 31)) & 1u) == 0u;  // filtered: bias −1 and the true id, never above
-        }
-        const float s = acc[i][j][r];
-        const float st = sts[m];
-        const uint64_t bg = __ballot(ok && s > st);
-        const uint64_t be = __ballot(ok && s == st);
-        if (lane == 0) {
-          const int m_lo = wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2);
-          const int g0 = __popcll(bg & 0xffffffffull), g1 = __popcll(bg >> 32);
-          const int q0c = __popcll(be & 0xffffffffull), q1c = __popcll(be >> 32);
-          if (g0) atomicAdd(&cgt[m_lo], g0);
-          if (g1) atomicAdd(&cgt[m_lo + 4], g1);
-          if (q0c) atomicAdd(&ceq[m_lo], q0c);
-          if (q1c) atomicAdd(&ceq[m_lo + 4], q1c);
-        }
-      }
+    // lanes l and l + 32 hold the two row halves of the same query column
+    g += __shfl_xor(g, 32);
+    e_ += __shfl_xor(e_, 32);
+    if (kh == 0 && q >= 0) {
+      if (g) atomicAdd(&cgt[n], g);
+      if (e_) atomicAdd(&ceq[n], e_);
     }
+  }
   __syncthreads();
   if (t < 128 && arow[t] >= 0) {
     if (cgt[t]) atomicAdd(&a.gt[q0 + t], cgt[t]);
@@ -175,10 +209,14 @@ __global__ __launch_bounds__(256) void k_rank_mfma(MfmaArgs a) {
 
 // filtered-candidate bitmap from the CSR (one thread per filtered id)
 __global__ __launch_bounds__(256) void k_filter_bits(const int64_t* __restrict__ off, const int64_t* __restrict__ ids,
-                                                     int64_t nq, int64_t E, int64_t W, uint32_t* __restrict__ bits,
-                                                     int32_t* err) {
+                                                     const int64_t* __restrict__ true_id, int64_t nq, int64_t E,
+                                                     int64_t W, uint32_t* __restrict__ bits, int32_t* err) {
   const int64_t q = blockIdx.y;
   if (q >= nq) return;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {  // the true entity is never counted against itself
+    const int64_t t = true_id[q];
+    if (t >= 0 && t < E) atomicOr(&bits[q * W + (t >> 5)], 1u << (t & 31));
+  }
   const int64_t b = off[q], e_ = off[q + 1];
   for (int64_t p = b + (int64_t)blockIdx.x * 256 + threadIdx.x; p < e_; p += (int64_t)gridDim.x * 256) {
     const int64_t e = ids[p];
@@ -202,13 +240,14 @@ __global__ __launch_bounds__(256) void k_rank_emit(const int32_t* __restrict__ g
 
 }  // namespace
 
-int launch_filter_bits(const int64_t* filt_off, const int64_t* filt_ids, int64_t nq, int64_t E, uint32_t* bits,
-                       int32_t* err, hipStream_t s) {
+int launch_filter_bits(const int64_t* filt_off, const int64_t* filt_ids, const int64_t* true_id, int64_t nq,
+                       int64_t E, uint32_t* bits, int32_t* err, hipStream_t s) {
   const int64_t W = (E + 31) / 32;
   hipError_t he = hipMemsetAsync(bits, 0, (size_t)nq * W * 4, s);
   if (he != hipSuccess) return (int)he;
   if (nq > 65535) return -1;
-  hipLaunchKernelGGL(k_filter_bits, dim3(4, (unsigned)nq), dim3(256), 0, s, filt_off, filt_ids, nq, E, W, bits, err);
+  hipLaunchKernelGGL(k_filter_bits, dim3(4, (unsigned)nq), dim3(256), 0, s, filt_off, filt_ids, true_id, nq, E, W,
+                     bits, err);
   return (int)hipGetLastError();
 }
 
@@ -224,7 +263,7 @@ int launch_rank_mfma(const float* q, const float* ent, int64_t nq, int64_t E, in
                      float* s_true, const int64_t* filt_off, const int64_t* filt_ids, uint32_t* bits, int32_t* gt,
                      int32_t* eq, int64_t* ranks, int32_t* ties, int32_t* err, hipStream_t s) {
   const int64_t W = (E + 31) / 32;
-  int st = launch_filter_bits(filt_off, filt_ids, nq, E, bits, err, s);
+  int st = launch_filter_bits(filt_off, filt_ids, true_id, nq, E, bits, err, s);
   if (st) return st;
   MfmaArgs a;
   a.q = q; a.ent = ent; a.nq = nq; a.E = E; a.K = K; a.true_id = true_id; a.s_true = s_true;
