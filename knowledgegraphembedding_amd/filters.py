@@ -16,16 +16,25 @@ import numpy as np
 class FilterIndex:
     def __init__(self, all_true_triples, nentity: int, nrelation: int):
         t = np.asarray(all_true_triples, dtype=np.int64).reshape(-1, 3)
-        t = np.unique(t, axis=0)  # set(all_true_triples), dataloader.py:125
         self.nentity = int(nentity)
         self.nrelation = int(nrelation)
         R, E = self.nrelation, self.nentity
-        k_hr = t[:, 0] * R + t[:, 1]
-        o = np.lexsort((t[:, 2], k_hr))
-        self._k_hr, self._tails = k_hr[o], t[o, 2]
-        k_rt = t[:, 1] * E + t[:, 2]
-        o = np.lexsort((t[:, 0], k_rt))
-        self._k_rt, self._heads = k_rt[o], t[o, 0]
+        if R * E * E < 2 ** 62:
+            # set(all_true_triples) (dataloader.py:125) and both orders as sorts
+            # of packed int64 keys: ((h·R + r)·E + t) and ((r·E + t)·E + h)
+            hr_t = np.unique((t[:, 0] * R + t[:, 1]) * E + t[:, 2])
+            self._k_hr, self._tails = hr_t // E, hr_t % E
+            h, r = self._k_hr // R, self._k_hr % R
+            rt_h = np.sort((r * E + self._tails) * E + h)
+            self._k_rt, self._heads = rt_h // E, rt_h % E
+        else:
+            t = np.unique(t, axis=0)
+            k_hr = t[:, 0] * R + t[:, 1]
+            o = np.lexsort((t[:, 2], k_hr))
+            self._k_hr, self._tails = k_hr[o], t[o, 2]
+            k_rt = t[:, 1] * E + t[:, 2]
+            o = np.lexsort((t[:, 0], k_rt))
+            self._k_rt, self._heads = k_rt[o], t[o, 0]
 
     def filter_csr(self, queries, mode: str):
         """(offsets [nq+1] int64, ids int64) of the filtered candidates per query."""

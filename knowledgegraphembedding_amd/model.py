@@ -436,11 +436,14 @@ class KGEModel(nn.Module):
         index = FilterIndex(all_true_triples, args.nentity, args.nrelation)
         triples = np.asarray(test_triples, dtype=np.int64).reshape(-1, 3)
         desc = model.desc()
-        logs = []
+        ranks_seq = []  # head-batch queries, then tail-batch, as the reference's logs list
         test_batch_size = max(1, int(args.test_batch_size))
         total_steps = 2 * ((len(triples) + test_batch_size - 1) // test_batch_size)
         test_log_steps = max(1, int(getattr(args, 'test_log_steps', 1000)))
-        block = max(test_batch_size, 256)  # queries per kernel launch; results do not depend on it
+        # queries per kernel launch (results do not depend on it): as many as
+        # keep the per-launch q buffer and filter bitmap within 128 MB each
+        row_bytes = max(4 * int(model.entity_dim), 4 * ((int(args.nentity) + 31) // 32))
+        block = max(test_batch_size, min(16384, max(256, (128 << 20) // row_bytes)))
         step = 0
         with torch.no_grad():
             for mode in ('head-batch', 'tail-batch'):
@@ -459,18 +462,17 @@ class KGEModel(nn.Module):
                         step += 1
                 ranks_np = torch.cat(ranks_all).cpu().numpy() if ranks_all else np.zeros(0, np.int64)
                 ops.raise_on_device_error(dev)
-                for ranking in ranks_np.tolist():
-                    logs.append({
-                        'MRR': 1.0 / ranking,
-                        'MR': float(ranking),
-                        'HITS@1': 1.0 if ranking <= 1 else 0.0,
-                        'HITS@3': 1.0 if ranking <= 3 else 0.0,
-                        'HITS@10': 1.0 if ranking <= 10 else 0.0,
-                    })
-        metrics = {}
-        for metric in logs[0].keys():
-            metrics[metric] = sum([log[metric] for log in logs]) / len(logs)
-        return metrics
+                ranks_seq.extend(ranks_np.tolist())
+        # model.py:405-427: per-query log entries averaged in order — the same
+        # left-to-right float sums, without materialising a dict per query
+        n = len(ranks_seq)
+        return {
+            'MRR': sum(1.0 / r for r in ranks_seq) / n,
+            'MR': sum(float(r) for r in ranks_seq) / n,
+            'HITS@1': sum(1.0 if r <= 1 else 0.0 for r in ranks_seq) / n,
+            'HITS@3': sum(1.0 if r <= 3 else 0.0 for r in ranks_seq) / n,
+            'HITS@10': sum(1.0 if r <= 10 else 0.0 for r in ranks_seq) / n,
+        }
 
     def rank_queries(self, triples, all_true_triples, mode):
         """Per-query filtered ranks and tie counts (numpy int64, int32) — the

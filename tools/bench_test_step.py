@@ -1,0 +1,66 @@
+#!/usr/bin/env python3
+"""KGEModel.test_step end to end at the FB15k evaluation shape (the
+reference's filtered MRR/MR/HITS pass, model.py:315-429): E=14951, R=1345,
+RotatE d=1000 -de, 483,142 train + 50,000 valid + 59,071 test synthetic
+triples (all_true = their union), test_batch_size 16 (best_config.sh:3).
+Reports wall seconds and queries/s (both directions), plus the host time of
+the filter index build.
+
+    python tools/bench_test_step.py [--model RotatE] [--test 59071]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+from argparse import Namespace
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from knowledgegraphembedding_amd import KGEModel, synth  # noqa: E402
+from knowledgegraphembedding_amd.filters import FilterIndex  # noqa: E402
+
+E, R = 14951, 1345
+DIMS = {"RotatE": (True, False), "TransE": (False, False), "DistMult": (False, False), "ComplEx": (True, True),
+        "pRotatE": (False, False)}
+
+
+def triples(seed, n):
+    return np.stack([synth.randint(seed, (n,), E), synth.randint(seed + 1, (n,), R),
+                     synth.randint(seed + 2, (n,), E)], 1).astype(np.int64)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--model", default="RotatE")
+    ap.add_argument("--test", type=int, default=59071)
+    ap.add_argument("-d", "--hidden_dim", type=int, default=1000)
+    a = ap.parse_args()
+    train, valid, test = triples(11, 483142), triples(21, 50000), triples(31, a.test)
+    all_true = np.concatenate([train, valid, test])
+    de, dr = DIMS[a.model]
+    torch.manual_seed(0)
+    m = KGEModel(a.model, E, R, a.hidden_dim, 24.0, de, dr).cuda()
+    args = Namespace(countries=False, nentity=E, nrelation=R, test_batch_size=16, cpu_num=10,
+                     test_log_steps=10 ** 9, cuda=True)
+    # warm-up (small) — builds kernels' first-use state
+    KGEModel.test_step(m, test[:64], all_true, args)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    FilterIndex(all_true, E, R)
+    t_index = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    met = KGEModel.test_step(m, test, all_true, args)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    nq = 2 * len(test)
+    print(json.dumps({"model": a.model, "hidden_dim": a.hidden_dim, "entities": E, "queries": nq,
+                      "seconds": dt, "queries_per_s": nq / dt, "filter_index_build_s": t_index,
+                      "metrics": met}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
