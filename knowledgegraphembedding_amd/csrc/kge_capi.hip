@@ -239,7 +239,7 @@ int run_grad(const kge_model_desc* m, const Geom& geo, int mode, const int64_t* 
   // 16-B slot per lane per slice; KGE_ENT_SLICES=0 selects the row-per-wave pass
   int nsl = 0;
   {
-    static const int forced = env_int("KGE_ENT_SLICES", -1);
+    const int forced = env_int("KGE_ENT_SLICES", -1);  // read per call (tests switch it)
     const int S = geo.eg.S;
     auto fits = [&](int k) { return (S + k - 1) / k <= 64; };
     if (geo.vec == 4 && forced != 0) {

@@ -44,12 +44,12 @@ def _batches(dev):
     return out
 
 
-def _args(group):
+def _args(group, reg=0.0):
     return Namespace(cuda=True, negative_adversarial_sampling=True, adversarial_temperature=1.0, uni_weight=False,
-                     regularization=0.0, dp_group=group)
+                     regularization=reg, dp_group=group)
 
 
-def _worker(rank, world, port, name, out):
+def _worker(rank, world, port, name, reg, out):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     torch.cuda.set_device(0)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -59,22 +59,22 @@ def _worker(rank, world, port, name, out):
     opt = KGEAdam(part.parameters(), lr=LR)
     sl = slice(rank * B // world, (rank + 1) * B // world)
     it = iter([(p[sl], n[sl], w[sl], m) for p, n, w, m in _batches("cuda:0")])
-    logs = [KGEModel.train_step(model, opt, it, _args(dist.group.WORLD)) for _ in range(2)]
+    logs = [KGEModel.train_step(model, opt, it, _args(dist.group.WORLD, reg)) for _ in range(2)]
     torch.cuda.synchronize()
     out[rank] = {"logs": logs, "ent": model.entity_embedding.detach().cpu().numpy(),
                  "rel": model.relation_embedding.detach().cpu().numpy()}
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("name", ["RotatE", "pRotatE"])
-def test_row_partition_two_ranks_on_gpu(name):
+@pytest.mark.parametrize("name,reg", [("RotatE", 0.0), ("pRotatE", 0.0), ("ComplEx", 1e-4)])
+def test_row_partition_two_ranks_on_gpu(name, reg):
     world = 2
     out = mp.Manager().dict()
-    mp.spawn(_worker, args=(world, _free_port(), name, out), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), name, reg, out), nprocs=world, join=True)
     model = _model(name)
     opt = KGEAdam([p for p in model.parameters() if p.requires_grad], lr=LR)
     it = iter(_batches("cuda:0"))
-    ref = [KGEModel.train_step(model, opt, it, _args(None)) for _ in range(2)]
+    ref = [KGEModel.train_step(model, opt, it, _args(None, reg)) for _ in range(2)]
     ent = model.entity_embedding.detach().cpu().numpy()
     rel = model.relation_embedding.detach().cpu().numpy()
     for rank in range(world):
@@ -82,5 +82,5 @@ def test_row_partition_two_ranks_on_gpu(name):
         np.testing.assert_allclose(r["ent"], ent, rtol=1e-5, atol=2e-6)
         np.testing.assert_allclose(r["rel"], rel, rtol=1e-5, atol=2e-6)
         for got, want in zip(r["logs"], ref):
-            for k in ("positive_sample_loss", "negative_sample_loss", "loss"):
+            for k in ("positive_sample_loss", "negative_sample_loss", "loss") + (("regularization",) if reg else ()):
                 np.testing.assert_allclose(got[k], want[k], rtol=2e-5)
