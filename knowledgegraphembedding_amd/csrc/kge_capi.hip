@@ -231,9 +231,6 @@ int run_grad(const kge_model_desc* m, const Geom& geo, int mode, const int64_t* 
   int st;
 
   const Schedule& sch = schedule();
-  // relation pass beside the entity pass; in phased calls always on the side
-  // stream (or, with no side stream, right after the epilogue)
-  const bool rel_side = sd && (!sch.rel_main || !all);
 
   // entity pass variant: column slices (k_entity_sl) when the row fits one
   // 16-B slot per lane per slice; KGE_ENT_SLICES=0 selects the row-per-wave pass
@@ -253,6 +250,11 @@ int run_grad(const kge_model_desc* m, const Geom& geo, int mode, const int64_t* 
     }
   }
   const int64_t ent_parts = m->nentity * (int64_t)(nsl > 0 ? nsl : 1);
+  // relation pass: as trailing blocks of the sliced entity launch (one call,
+  // no stream join); else beside the entity pass on the side stream (always
+  // so in phased calls), or on the caller's stream
+  const bool rel_fused = all && nsl > 0 && env_int("KGE_REL_FUSED", 1) != 0;
+  const bool rel_side = sd && !rel_fused && (!sch.rel_main || !all);
   RelArgs rl;
   rl.rel = m->relation_embedding; rl.R = m->nrelation; rl.E = m->nentity; rl.B = B; rl.Bn = B * n; rl.Lr = Lr;
   rl.off = w.off; rl.occ = w.occ; rl.rel_contrib = w.rel_contrib; rl.reg3 = 3.f * reg;
@@ -327,6 +329,8 @@ int run_grad(const kge_model_desc* m, const Geom& geo, int mode, const int64_t* 
   ea.slice_w = nsl > 0 ? (geo.eg.S + nsl - 1) / nsl : 0;
   ea.adam = adam_t(adam ? &adam->entity : nullptr);
   ea.adamk = ak;
+  ea.rel = rl;
+  ea.rel_blocks = rel_fused ? (m->nrelation + 3) / 4 : 0;
   if (e_end > e_begin) {
     st = launch_status(op.entity(mode, geo.vec, geo.ns, ea, s));
     if (st) return st;
@@ -337,7 +341,7 @@ int run_grad(const kge_model_desc* m, const Geom& geo, int mode, const int64_t* 
   if (!(phases & KGE_PHASE_FINALIZE)) return KGE_OK;
   if (rel_side) {
     hipStreamWaitEvent(s, sd->rel_done, 0);  // join 2: everything the side stream wrote
-  } else if (all) {
+  } else if (all && !rel_fused) {
     st = launch_status(launch_rel_rows(rl, s));
     if (st) return st;
   }

@@ -17,20 +17,6 @@ struct CsrArgs {
   int32_t* err;
 };
 
-struct RelArgs {
-  const float* rel;
-  int64_t R, E, B, Bn;
-  int Lr;
-  const int32_t* off;
-  const int32_t* occ;
-  const float* rel_contrib;  // [B, Lr]
-  float reg3;
-  float* reg_partial;        // [R]
-  float* grad_rel;
-  int write_grad;            // store grad_rel (always, unless the optimizer is fused and asks not to)
-  AdamT adam;                // fused optimizer step (adam.p == null: none)
-  AdamK adamk;
-};
 
 struct FinArgs {
   const float* row_stats;    // [B, 4]

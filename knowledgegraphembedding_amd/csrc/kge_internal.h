@@ -60,6 +60,21 @@ struct RowArgs {
   void (*timer_mid)(hipStream_t);  // stage-timer hook between the row-pass launches (or null)
 };
 
+struct RelArgs {
+  const float* rel;
+  int64_t R, E, B, Bn;
+  int Lr;
+  const int32_t* off;
+  const int32_t* occ;
+  const float* rel_contrib;  // [B, Lr]
+  float reg3;
+  float* reg_partial;        // [R]
+  float* grad_rel;
+  int write_grad;            // store grad_rel (always, unless the optimizer is fused and asks not to)
+  AdamT adam;                // fused optimizer step (adam.p == null: none)
+  AdamK adamk;
+};
+
 struct EntArgs {
   const float* ent;
   const float* modulus;
@@ -85,6 +100,8 @@ struct EntArgs {
   int slice_w;
   AdamT adam;           // fused optimizer step (adam.p == null: none)
   AdamK adamk;
+  RelArgs rel;          // rel_blocks > 0: trailing blocks of k_entity_sl run the relation pass
+  int64_t rel_blocks;
 };
 
 struct RankArgs {
