@@ -323,7 +323,7 @@ int run_grad(const kge_model_desc* m, const Geom& geo, int mode, const int64_t* 
   ea.minw = ent_minw;
   ea.nsl = nsl;
   if (nsl > 0) {
-    static const int pf = env_int("KGE_ENT_PF", 5);  // 5: 4 rows in flight + Adam moments loaded up front (measured best)
+    static const int pf = env_int("KGE_ENT_PF", 6);  // 6: 4 rows in flight, Adam moments up front, packed RotatE math (measured best)
     ea.minw = pf;
   }
   ea.slice_w = nsl > 0 ? (geo.eg.S + nsl - 1) / nsl : 0;

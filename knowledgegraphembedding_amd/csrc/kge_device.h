@@ -48,6 +48,8 @@ struct Consts {
 };
 
 // ---------------------------------------------------------------- loads
+typedef float tf2 __attribute__((ext_vector_type(2)));  // a register pair (v_pk_*_f32 operand)
+
 template <int VEC>
 __device__ __forceinline__ void ldv(const float* __restrict__ p, float (&x)[VEC]) {
   if constexpr (VEC == 4) {
