@@ -375,6 +375,7 @@ RowArgs row_args(const kge_model_desc* m, const Geom& geo, const int64_t* pos, c
     return e ? atoi(e) : 0;
   }();
   ra.pipe = pipe;
+  ra.fuse_q = env_int("KGE_FUSE_Q", 1);  // measured +1.8 %; bit-identical to the separate k_build_q
   return ra;
 }
 

@@ -462,3 +462,32 @@ def test_entity_pass_column_slices_bitwise(name, monkeypatch):
         for (l0, g0, p0), (l1, g1, p1) in zip(out["0"], out[nsl]):
             assert torch.equal(g0, g1) and torch.equal(p0, p1), nsl
             torch.testing.assert_close(l0[:4], l1[:4], rtol=1e-6, atol=0)
+
+
+@pytest.mark.parametrize("name", NAMES)
+def test_fused_q_build_bitwise(name, monkeypatch):
+    """k_row building q and Σw in its own prologue (KGE_FUSE_Q=1) gives the
+    separate k_build_q launch's losses, gradients and q-dependent results bit
+    for bit (same per-element q arithmetic, same fixed-order Σw reduction)."""
+    E, R, d, B, n = 400, 9, 120, 24, 40
+    pos, neg, w = synth.kge_batch(91, B, n, E, R)
+    P, N, W = torch.from_numpy(pos).to(DEV), torch.from_numpy(neg).to(DEV), torch.from_numpy(w).to(DEV)
+    res = {}
+    for fq in ("0", "1"):
+        monkeypatch.setenv("KGE_FUSE_Q", fq)
+        out = []
+        for adv, uni in ((True, False), (False, True)):
+            m, *_ = build_model(name, E, R, d, 12.0, 7)
+            args = Namespace(negative_adversarial_sampling=adv, adversarial_temperature=0.7, uni_weight=uni,
+                             regularization=0.0)
+            for mode in ("tail-batch", "head-batch"):
+                losses = m.compute_train_grads(P, N, W, mode, args)
+                out.append([t.detach().cpu().clone() for t in (losses, m.entity_embedding.grad,
+                                                               m.relation_embedding.grad)])
+            # Σw supplied by the caller (the data-parallel path)
+            losses = m.compute_train_grads(P, N, W, "tail-batch", args, weight_sum=W.sum().reshape(1))
+            out.append([losses.detach().cpu().clone(), m.entity_embedding.grad.cpu().clone()])
+        res[fq] = out
+    for a, b in zip(res["0"], res["1"]):
+        for x, y in zip(a, b):
+            assert torch.equal(x, y)
