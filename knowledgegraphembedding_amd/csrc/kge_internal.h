@@ -56,7 +56,8 @@ struct RowArgs {
   float* row_stats;   // [B, 4]  logσ(s_pos), neg term, d/dmodulus, s_pos
   int n_lds;          // floats reserved for raw scores in LDS (TRAIN: n)
   int pipe;           // k_row variant: 1 = next row prefetched (3 waves/SIMD), 0 = 4 waves/SIMD
-  int fuse_q;         // 1: k_row builds q (and Σw) itself, no k_build_q launch (ROW_TRAIN only)
+  int fuse_q;         // 1: k_row builds q (and Σw) itself, no k_build_q launch
+  int fuse_epi;       // 1 (with fuse_q): k_row runs the epilogue in its tail, no k_row_epi launch
   int32_t* err;
   void (*timer_mid)(hipStream_t);  // stage-timer hook between the row-pass launches (or null)
 };

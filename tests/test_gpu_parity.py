@@ -466,15 +466,17 @@ def test_entity_pass_column_slices_bitwise(name, monkeypatch):
 
 @pytest.mark.parametrize("name", NAMES)
 def test_fused_q_build_bitwise(name, monkeypatch):
-    """k_row building q and Σw in its own prologue (KGE_FUSE_Q=1) gives the
-    separate k_build_q launch's losses, gradients and q-dependent results bit
-    for bit (same per-element q arithmetic, same fixed-order Σw reduction)."""
+    """k_row building q and Σw in its own prologue (KGE_FUSE_Q=1), and also
+    running the epilogue in its tail (KGE_FUSE_EPI=1), give the separate
+    launches' losses and gradients bit for bit (same per-element arithmetic,
+    same fixed-order Σw reduction, same epilogue function)."""
     E, R, d, B, n = 400, 9, 120, 24, 40
     pos, neg, w = synth.kge_batch(91, B, n, E, R)
     P, N, W = torch.from_numpy(pos).to(DEV), torch.from_numpy(neg).to(DEV), torch.from_numpy(w).to(DEV)
     res = {}
-    for fq in ("0", "1"):
-        monkeypatch.setenv("KGE_FUSE_Q", fq)
+    for fq in ("0", "1", "epi"):
+        monkeypatch.setenv("KGE_FUSE_Q", "0" if fq == "0" else "1")
+        monkeypatch.setenv("KGE_FUSE_EPI", "1" if fq == "epi" else "0")
         out = []
         for adv, uni in ((True, False), (False, True)):
             m, *_ = build_model(name, E, R, d, 12.0, 7)
@@ -488,6 +490,7 @@ def test_fused_q_build_bitwise(name, monkeypatch):
             losses = m.compute_train_grads(P, N, W, "tail-batch", args, weight_sum=W.sum().reshape(1))
             out.append([losses.detach().cpu().clone(), m.entity_embedding.grad.cpu().clone()])
         res[fq] = out
-    for a, b in zip(res["0"], res["1"]):
-        for x, y in zip(a, b):
-            assert torch.equal(x, y)
+    for variant in ("1", "epi"):
+        for a, b in zip(res["0"], res[variant]):
+            for x, y in zip(a, b):
+                assert torch.equal(x, y), variant
