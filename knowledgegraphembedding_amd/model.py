@@ -147,12 +147,24 @@ class _LogRing:
                        None] for _ in range(depth)]
         self.k = 0
 
+    def reserve(self) -> torch.Tensor:
+        """The next slot's pinned [5] buffer (its previous log completed first):
+        the single-device step's k_finalize writes the losses straight into it."""
+        slot = self.slots[self.k]
+        if slot[2] is not None:
+            slot[2]._fill()
+            slot[2] = None
+        return slot[0]
+
     def push(self, losses: torch.Tensor, has_reg: bool) -> StepLog:
+        """Log of the step whose losses are in `losses` (copied unless it is the
+        reserved slot itself); the event marks when the slot holds them."""
         slot = self.slots[self.k]
         self.k = (self.k + 1) % len(self.slots)
         if slot[2] is not None:
             slot[2]._fill()
-        slot[0].copy_(losses, non_blocking=True)
+        if losses.data_ptr() != slot[0].data_ptr():
+            slot[0].copy_(losses, non_blocking=True)
         if slot[1] is not None:
             slot[1].record()
         log = StepLog((slot[0], slot[1], has_reg, self.dev))
@@ -314,8 +326,21 @@ class KGEModel(nn.Module):
             self._grad_bufs = bufs = (ge, gr, gm, losses)
         return bufs
 
+    def _log_ring_for(self, dev):
+        ring = self.__dict__.get('_log_ring')
+        if ring is None or ring.dev != dev:
+            ring = self.__dict__['_log_ring'] = _LogRing(dev)
+        return ring
+
+    def _log_slot(self, dev):
+        """Pinned host buffer the next step's losses are written to (None off-GPU)."""
+        if dev.type != 'cuda' or not self.defer_log:
+            return None
+        return self._log_ring_for(dev).reserve()
+
     def compute_train_grads(self, positive_sample, negative_sample, subsampling_weight, mode, args,
-                            weight_sum=None, uni_batch=0, optimizer=None, entity_chunks=None, on_entity_chunk=None):
+                            weight_sum=None, uni_batch=0, optimizer=None, entity_chunks=None, on_entity_chunk=None,
+                            losses_out=None):
         """Fused forward + self-adversarial loss + backward (model.py:268-301).
         Writes dense .grad tensors; returns the device [5] vector
         (positive_sample_loss, negative_sample_loss, loss, regularization, error flag).
@@ -328,6 +353,8 @@ class KGEModel(nn.Module):
         dev = ops._require_device(self.entity_embedding)
         g, rng = self._host_scalars()
         ge, gr, gm, losses = self._grad_buffers()
+        if losses_out is not None:  # e.g. a pinned host slot the kernels write directly
+            losses = losses_out
         adam = None
         if optimizer is not None and self.fuse_optimizer and hasattr(optimizer, 'prepare_fused'):
             adam = optimizer.prepare_fused(self.entity_embedding, self.relation_embedding, self._modulus(),
@@ -388,20 +415,18 @@ class KGEModel(nn.Module):
                                     optimizer=optimizer)
         else:
             # a KGEAdam optimizer is stepped inside the gradient passes; any
-            # other optimizer sees ordinary dense .grad tensors
+            # other optimizer sees ordinary dense .grad tensors.  The loss
+            # vector goes straight into the next pinned log slot (no D2H copy)
             losses = model.compute_train_grads(positive_sample, negative_sample, subsampling_weight, mode, args,
-                                               optimizer=optimizer)
+                                               optimizer=optimizer, losses_out=model._log_slot(dev))
 
         optimizer.step()
         if part is not None:
             part.gather()  # owners' updated rows → every replica
 
-        # the step's only device→host transfer: 4 losses + the error flag into
-        # a pinned slot; the log reads it on first access (StepLog)
-        ring = model.__dict__.get('_log_ring')
-        if ring is None or ring.dev != dev:
-            ring = model.__dict__['_log_ring'] = _LogRing(dev)
-        log = ring.push(losses, args.regularization != 0.0)
+        # the step's only device→host transfer: 4 losses + the error flag in a
+        # pinned slot; the log reads it on first access (StepLog)
+        log = model._log_ring_for(dev).push(losses, args.regularization != 0.0)
         if not model.defer_log:
             log._fill()
         return log
