@@ -11,10 +11,11 @@
 // are produced by identical instruction sequences and compare consistently.
 //
 // Tile: 128 queries × 128 candidates per workgroup (4 waves as 2×2, each
-// 64×64 = 2×2 MFMA tiles), K staged through LDS 32 deep, transposed to
-// [k][row] (rows padded to 132 floats) so each lane's A/B operand is one
-// ds_read_b32; the next slab's global loads are issued into registers before
-// the current slab's MFMAs, so their latency hides behind the matrix work.
+// 64×64 = 2×2 MFMA tiles), K staged through LDS 32 deep, rows kept row-major
+// with each 8-k group permuted into MFMA consumption order, so one
+// ds_read_b128 per operand feeds four k-steps; the next slab's global loads
+// are issued into registers before the current slab's MFMAs, so their
+// latency hides behind the matrix work.
 // Candidates are the MFMA rows and queries the columns, so each lane owns two
 // query columns: the epilogue tests its 32 candidates per query against s_true
 // and a 2-word slice of the query's exclusion bitmap (filtered ids, the true
@@ -30,7 +31,10 @@ namespace {
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 constexpr int BM = 128, BN = 128, BK = 32;
-constexpr int LDW = 128 + 4;  // padded LDS row: the transposed float4 stores hit 4 bank groups
+// LDS slab: row-major [128 rows][LDK], each group of 8 k stored in MFMA
+// consumption order [k0, k0+2, k0+4, k0+6 | k0+1, k0+3, k0+5, k0+7] so one
+// ds_read_b128 gives a lane (row li, half kh) its operands for 4 k-steps.
+constexpr int LDK = BK + 4;
 constexpr int F4 = (BM * BK / 4) / 256;  // float4 per thread per operand per slab
 
 struct MfmaArgs {
@@ -70,22 +74,22 @@ __device__ __forceinline__ void fetch(float4 (&r)[F4], const float* __restrict__
     r[u] = v;
   }
 }
-__device__ __forceinline__ void put(float (*dst)[LDW], const float4 (&r)[F4], int t) {
+__device__ __forceinline__ void put(float (*dst)[LDK], const float4 (&r)[F4], int t) {
 #pragma unroll
   for (int u = 0; u < F4; ++u) {
     const int f = t + 256 * u;
     const int row = f / (BK / 4), kq = (f % (BK / 4)) * 4;
-    dst[kq + 0][row] = r[u].x;
-    dst[kq + 1][row] = r[u].y;
-    dst[kq + 2][row] = r[u].z;
-    dst[kq + 3][row] = r[u].w;
+    // k = kq..kq+3 → positions (k & 1)·4 + ((k & 7) >> 1) inside the 8-group
+    const int base = (kq & ~7) + ((kq & 4) ? 2 : 0);
+    *reinterpret_cast<float2*>(&dst[row][base]) = make_float2(r[u].x, r[u].z);
+    *reinterpret_cast<float2*>(&dst[row][base + 4]) = make_float2(r[u].y, r[u].w);
   }
 }
 
-template <bool GATHER>
-__global__ __launch_bounds__(256, 3) void k_rank_mfma(MfmaArgs a) {
-  __shared__ __attribute__((aligned(16))) float As[BK][LDW];
-  __shared__ __attribute__((aligned(16))) float Bs[BK][LDW];
+template <bool GATHER, int MINW>
+__global__ __launch_bounds__(256, MINW) void k_rank_mfma(MfmaArgs a) {
+  __shared__ __attribute__((aligned(16))) float As[BM][LDK];
+  __shared__ __attribute__((aligned(16))) float Bs[BN][LDK];
   __shared__ int64_t arow[128], brow[128];
   __shared__ float sts[128];
   __shared__ int32_t cgt[128], ceq[128];
@@ -130,20 +134,28 @@ __global__ __launch_bounds__(256, 3) void k_rank_mfma(MfmaArgs a) {
       fetch(rb, a.ent, brow, a.K, k0 + BK, t);
     }
 #pragma unroll
-    for (int kk = 0; kk < BK / 2; ++kk) {
-      // k order: (k0 + 2kk) in lanes 0-31, (k0 + 2kk + 1) in lanes 32-63 —
-      // ascending k across the loop, the same in both passes.  Candidates are
-      // the MFMA rows (A), queries the columns (B): a lane's accumulator
-      // column is one query, so the epilogue counts without cross-lane work.
-      float ef[2], qf[2];
+    for (int g = 0; g < BK / 8; ++g) {
+      // k order: step 4g + u takes k = k0 + 8g + 2u (lanes 0-31) and + 1
+      // (lanes 32-63) — ascending k across the loop, the same in both passes.
+      // Candidates are the MFMA rows (A), queries the columns (B): a lane's
+      // accumulator column is one query, so the epilogue counts per lane.
+      float4 e4[2], q4[2];
 #pragma unroll
-      for (int i = 0; i < 2; ++i) ef[i] = Bs[2 * kk + kh][wm * 64 + i * 32 + li];
+      for (int i = 0; i < 2; ++i) e4[i] = *reinterpret_cast<const float4*>(&Bs[wm * 64 + i * 32 + li][g * 8 + kh * 4]);
 #pragma unroll
-      for (int j = 0; j < 2; ++j) qf[j] = As[2 * kk + kh][wn * 64 + j * 32 + li];
+      for (int j = 0; j < 2; ++j) q4[j] = *reinterpret_cast<const float4*>(&As[wn * 64 + j * 32 + li][g * 8 + kh * 4]);
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+      for (int u = 0; u < 4; ++u) {
+        const float ef[2] = {u == 0 ? e4[0].x : u == 1 ? e4[0].y : u == 2 ? e4[0].z : e4[0].w,
+                             u == 0 ? e4[1].x : u == 1 ? e4[1].y : u == 2 ? e4[1].z : e4[1].w};
+        const float qf[2] = {u == 0 ? q4[0].x : u == 1 ? q4[0].y : u == 2 ? q4[0].z : q4[0].w,
+                             u == 0 ? q4[1].x : u == 1 ? q4[1].y : u == 2 ? q4[1].z : q4[1].w};
 #pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(ef[i], qf[j], acc[i][j], 0, 0, 0);
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(ef[i], qf[j], acc[i][j], 0, 0, 0);
+      }
     }
     __syncthreads();
   }
@@ -269,8 +281,20 @@ int launch_rank_mfma(const float* q, const float* ent, int64_t nq, int64_t E, in
   a.q = q; a.ent = ent; a.nq = nq; a.E = E; a.K = K; a.true_id = true_id; a.s_true = s_true;
   a.fbits = bits; a.W = W; a.gt = gt; a.eq = eq;
   const unsigned gy = (unsigned)((nq + BM - 1) / BM);
-  hipLaunchKernelGGL(k_rank_mfma<true>, dim3(1, gy), dim3(256), 0, s, a);
-  hipLaunchKernelGGL(k_rank_mfma<false>, dim3((unsigned)((E + BN - 1) / BN), gy), dim3(256), 0, s, a);
+  // 3 waves/SIMD (158 VGPRs, no spills); 4 fits only with 13 spilled VGPRs
+  // and measured 12 % slower
+  static const int minw = [] {
+    const char* e = getenv("KGE_RANK_MFMA_MINW");
+    return e ? atoi(e) : 3;
+  }();
+  const dim3 gs((unsigned)((E + BN - 1) / BN), gy);
+  if (minw == 4) {
+    hipLaunchKernelGGL((k_rank_mfma<true, 4>), dim3(1, gy), dim3(256), 0, s, a);
+    hipLaunchKernelGGL((k_rank_mfma<false, 4>), gs, dim3(256), 0, s, a);
+  } else {
+    hipLaunchKernelGGL((k_rank_mfma<true, 3>), dim3(1, gy), dim3(256), 0, s, a);
+    hipLaunchKernelGGL((k_rank_mfma<false, 3>), gs, dim3(256), 0, s, a);
+  }
   st = (int)hipGetLastError();
   if (st) return st;
   return launch_rank_emit(gt, eq, true_id, nq, ranks, ties, s);
