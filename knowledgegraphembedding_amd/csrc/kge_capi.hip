@@ -107,6 +107,8 @@ struct Carver {
 struct GradWs {
   float *g, *q, *dq, *ent_contrib, *rel_contrib, *row_stats, *reg_partial, *wsum;
   int32_t *keys, *cnt, *off, *tmp, *occ;
+  void* scan_tmp;
+  size_t scan_tmp_bytes;
 };
 
 GradWs carve_grad(void* ws, const kge_model_desc* m, int64_t B, int64_t n, size_t* bytes) {
@@ -122,10 +124,12 @@ GradWs carve_grad(void* ws, const kge_model_desc* m, int64_t B, int64_t n, size_
   w.reg_partial = c.take<float>(8 * m->nentity + m->nrelation);  // per (entity, column slice) + per relation
   w.wsum = c.take<float>(4);
   w.keys = c.take<int32_t>(N);
-  w.cnt = c.take<int32_t>(nb);
+  w.cnt = c.take<int32_t>(nb + 1);
   w.off = c.take<int32_t>(nb + 1);
   w.tmp = c.take<int32_t>(N);
   w.occ = c.take<int32_t>(N);
+  w.scan_tmp_bytes = csr_scan_temp_bytes(nb);
+  w.scan_tmp = c.take<uint8_t>((int64_t)w.scan_tmp_bytes);
   *bytes = c.off + 256;
   return w;
 }
@@ -280,6 +284,7 @@ int run_grad(const kge_model_desc* m, const Geom& geo, int mode, const int64_t* 
   ca.pos = pos; ca.neg = neg; ca.neg_stride = neg_stride;
   ca.B = B; ca.n = n; ca.Bn = B * n; ca.E = m->nentity; ca.R = m->nrelation;
   ca.keys = w.keys; ca.cnt = w.cnt; ca.off = w.off; ca.tmp = w.tmp; ca.occ = w.occ; ca.err = err;
+  ca.scan_tmp = w.scan_tmp; ca.scan_tmp_bytes = w.scan_tmp_bytes;
   if (sd) hipStreamWaitEvent(ss, sd->fork, 0);
   st = launch_status(launch_csr(ca, ss));
   if (st) return st;

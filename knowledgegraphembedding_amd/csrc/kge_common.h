@@ -10,11 +10,13 @@ struct CsrArgs {
   int64_t neg_stride;
   int64_t B, n, Bn, E, R;
   int32_t* keys;  // [Bn + 3B]
-  int32_t* cnt;   // [E + R]
+  int32_t* cnt;   // [E + R + 1]  (last slot stays 0: the scan's total)
   int32_t* off;   // [E + R + 1]
   int32_t* tmp;   // [Bn + 3B]
   int32_t* occ;   // [Bn + 3B]
   int32_t* err;
+  void* scan_tmp;  // rocPRIM scan scratch (csr_scan_temp_bytes)
+  size_t scan_tmp_bytes;
 };
 
 
@@ -42,6 +44,7 @@ int launch_filter_bits(const int64_t* filt_off, const int64_t* filt_ids, const i
                        int64_t E, uint32_t* bits, int32_t* err, hipStream_t s);
 int launch_rank_emit(const int32_t* gt, const int32_t* eq, const int64_t* true_id, int64_t nq, int64_t* ranks,
                      int32_t* ties, hipStream_t s);
+size_t csr_scan_temp_bytes(int64_t nb);
 int launch_csr(const CsrArgs& a, hipStream_t s);
 int launch_rel_rows(const RelArgs& a, hipStream_t s);
 int launch_finalize(const FinArgs& a, hipStream_t s);

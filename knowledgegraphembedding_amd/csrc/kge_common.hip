@@ -1,5 +1,7 @@
 // kge_common.hip — model-independent kernels: occurrence CSR (deterministic
 // counting sort), relation-gradient row sums, loss finalisation, Σw and Adam.
+#include <rocprim/device/device_scan.hpp>
+
 #include "kge_common.h"
 #include "kge_rel.h"
 
@@ -35,31 +37,6 @@ __global__ __launch_bounds__(256) void k_csr_hist(CsrArgs a) {
     a.keys[k] = (int32_t)key;
     atomicAdd(&a.cnt[key], 1);
   }
-}
-
-// Exclusive scan of cnt[0..nb) into off[0..nb]; one workgroup of 1024 threads.
-__global__ __launch_bounds__(1024) void k_csr_scan(const int32_t* __restrict__ cnt, int32_t* __restrict__ off,
-                                                   int64_t nb) {
-  __shared__ int32_t part[1024];
-  const int tid = threadIdx.x;
-  const int64_t per = (nb + 1023) / 1024;
-  const int64_t b0 = tid * per, b1 = (b0 + per < nb) ? (b0 + per) : nb;
-  int32_t s = 0;
-  for (int64_t k = b0; k < b1; ++k) s += cnt[k];
-  part[tid] = s;
-  __syncthreads();
-  for (int o = 1; o < 1024; o <<= 1) {
-    const int32_t v = (tid >= o) ? part[tid - o] : 0;
-    __syncthreads();
-    part[tid] += v;
-    __syncthreads();
-  }
-  int32_t run = part[tid] - s;  // exclusive prefix of this thread's chunk
-  for (int64_t k = b0; k < b1; ++k) {
-    off[k] = run;
-    run += cnt[k];
-  }
-  if (tid == 1023) off[nb] = part[1023];
 }
 
 // Unordered fill: slot = off[key] + (--cnt[key]).
@@ -215,13 +192,31 @@ static inline unsigned grid_for(int64_t n, unsigned cap = 4096) {
   return (unsigned)(g < cap ? g : cap);
 }
 
+// Bucket offsets: a device-wide exclusive scan of cnt[0..nb] (cnt[nb] = 0, so
+// off[nb] = total) — rocPRIM's decoupled look-back scan, integer and exact;
+// its scratch comes from the caller's workspace.
+size_t csr_scan_temp_bytes(int64_t nb) {
+  static thread_local int64_t last_nb = -1;  // the query is per size; remember the last one
+  static thread_local size_t last_bytes = 0;
+  if (nb == last_nb) return last_bytes;
+  size_t bytes = 0;
+  if (rocprim::exclusive_scan(nullptr, bytes, (const int32_t*)nullptr, (int32_t*)nullptr, int32_t(0), (size_t)nb + 1,
+                              rocprim::plus<int32_t>()) != hipSuccess)
+    bytes = 0;
+  last_nb = nb;
+  last_bytes = bytes;
+  return bytes;
+}
+
 int launch_csr(const CsrArgs& a, hipStream_t s) {
   const int64_t nb = a.E + a.R;
   const int64_t N = a.Bn + 3 * a.B;
-  hipError_t e = hipMemsetAsync(a.cnt, 0, sizeof(int32_t) * nb, s);
+  hipError_t e = hipMemsetAsync(a.cnt, 0, sizeof(int32_t) * (nb + 1), s);
   if (e != hipSuccess) return (int)e;
   hipLaunchKernelGGL(k_csr_hist, dim3(grid_for(N)), dim3(256), 0, s, a);
-  hipLaunchKernelGGL(k_csr_scan, dim3(1), dim3(1024), 0, s, a.cnt, a.off, nb);
+  size_t bytes = a.scan_tmp_bytes;
+  e = rocprim::exclusive_scan(a.scan_tmp, bytes, a.cnt, a.off, int32_t(0), (size_t)nb + 1, rocprim::plus<int32_t>(), s);
+  if (e != hipSuccess) return (int)e;
   hipLaunchKernelGGL(k_csr_fill, dim3(grid_for(N)), dim3(256), 0, s, a);
   hipLaunchKernelGGL(k_csr_rank, dim3(grid_for(N)), dim3(256), 0, s, a);
   return (int)hipGetLastError();
