@@ -18,6 +18,6 @@ if [ "${PMC:-1}" = "1" ]; then
 fi
 if [ "${PMC:-1}" = "1" ]; then
   python3 "$ROOT/tools/pmc_traffic.py" "$OUT" --kernel k_row -o "$OUT/pmc_traffic.json" > /dev/null &&
-  python3 "$ROOT/tools/pmc_traffic.py" "$OUT" --kernel k_entity -o "$OUT/pmc_traffic_entity.json" > /dev/null
+  python3 "$ROOT/tools/pmc_traffic.py" "$OUT" --kernel k_entity_sl -o "$OUT/pmc_traffic_entity.json" > /dev/null
 fi
 find "$OUT" -name "*.csv" | head -20
