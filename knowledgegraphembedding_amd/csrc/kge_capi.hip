@@ -228,7 +228,11 @@ int run_grad(const kge_model_desc* m, const Geom& geo, int mode, const int64_t* 
   if (lds > 64 * 1024) return KGE_ERR_DIM;
   const bool all = (phases == KGE_PHASE_ALL);
   if (e_end < 0) e_end = m->nentity;
-  const bool timed = all && g_timer.on && ra.op == ROW_TRAIN && (g_timer.seen++ % (size_t)g_timer.period) == 0;
+  // stage timing: a full call records all 7 marks; a phased ROWS call (the
+  // data-parallel path) records the row-pass marks and pads the rest, so the
+  // row pass is timed live on every rank either way
+  const bool timed = (phases & KGE_PHASE_ROWS) && g_timer.on && ra.op == ROW_TRAIN &&
+                     (g_timer.seen++ % (size_t)g_timer.period) == 0;
   ra.timer_mid = timed ? &timer_mark : nullptr;
   Side* sd = side_for_device();
   hipStream_t ss = sd ? sd->s : s;
@@ -307,6 +311,8 @@ int run_grad(const kge_model_desc* m, const Geom& geo, int mode, const int64_t* 
     st = launch_status(launch_rel_rows(rl, s));
     if (st) return st;
   }
+  if (timed && !all)
+    for (int k = 0; k < 3; ++k) g_timer.mark(s);  // stages 3-5 not in this call
   }  // KGE_PHASE_ROWS
 
   if (phases & KGE_PHASE_ENTITY) {
