@@ -107,9 +107,26 @@ struct Carver {
 struct GradWs {
   float *g, *q, *dq, *ent_contrib, *rel_contrib, *row_stats, *reg_partial, *wsum;
   int32_t *keys, *cnt, *off, *tmp, *occ;
+  int2* meta;
   void* scan_tmp;
   size_t scan_tmp_bytes;
 };
+
+// Column tiles of the LDS-tiled entity pass (k_entity_tl): 16 complex dims
+// or 32 real dims per tile.
+int ent_tiles(const kge_model_desc* m) {
+  const bool cplx = (m->model == KGE_COMPLEX || m->model == KGE_ROTATE);
+  return cplx ? (m->entity_dim / 2 + 15) / 16 : (m->entity_dim + TL_COLS - 1) / TL_COLS;
+}
+int device_cus() {
+  static int n = [] {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0)
+      v = 256;
+    return v;
+  }();
+  return n;
+}
 
 GradWs carve_grad(void* ws, const kge_model_desc* m, int64_t B, int64_t n, size_t* bytes) {
   Carver c(ws);
@@ -121,13 +138,15 @@ GradWs carve_grad(void* ws, const kge_model_desc* m, int64_t B, int64_t n, size_
   w.ent_contrib = c.take<float>(2 * B * (int64_t)m->entity_dim);
   w.rel_contrib = c.take<float>(B * (int64_t)m->relation_dim);
   w.row_stats = c.take<float>(B * 4);
-  w.reg_partial = c.take<float>(8 * m->nentity + m->nrelation);  // per (entity, column slice) + per relation
+  const int64_t parts = ent_tiles(m) > 8 ? ent_tiles(m) : 8;
+  w.reg_partial = c.take<float>(parts * m->nentity + m->nrelation);  // per (entity, column slice/tile) + per relation
   w.wsum = c.take<float>(4);
   w.keys = c.take<int32_t>(N);
   w.cnt = c.take<int32_t>(nb + 1);
   w.off = c.take<int32_t>(nb + 1);
   w.tmp = c.take<int32_t>(N);
   w.occ = c.take<int32_t>(N);
+  w.meta = c.take<int2>(Bn + 2 * B);  // entity buckets only
   w.scan_tmp_bytes = csr_scan_temp_bytes(nb);
   w.scan_tmp = c.take<uint8_t>((int64_t)w.scan_tmp_bytes);
   *bytes = c.off + 256;
@@ -257,11 +276,17 @@ int run_grad(const kge_model_desc* m, const Geom& geo, int mode, const int64_t* 
       if ((k == 1 || k == 2 || k == 4 || k == 8) && fits(k)) nsl = k;
     }
   }
-  const int64_t ent_parts = m->nentity * (int64_t)(nsl > 0 ? nsl : 1);
+  // LDS-tiled entity pass (KGE_ENT_TILE=1, when the batch's q column tile fits
+  // in LDS): bit-identical, but measured slower than the sliced pass on the
+  // FB15k shape (0.34 vs 0.24 ms: 1.6x the VALU work — one complex dim per
+  // lane and 4-entity lockstep — outweighs the L2 gathers it removes)
+  int ntiles = 0;
+  if (env_int("KGE_ENT_TILE", 0) != 0 && B <= TL_MAX_ROWS) ntiles = ent_tiles(m);
+  const int64_t ent_parts = m->nentity * (int64_t)(ntiles > 0 ? ntiles : (nsl > 0 ? nsl : 1));
   // relation pass: as trailing blocks of the sliced entity launch (one call,
   // no stream join); else beside the entity pass on the side stream (always
   // so in phased calls), or on the caller's stream
-  const bool rel_fused = all && nsl > 0 && env_int("KGE_REL_FUSED", 1) != 0;
+  const bool rel_fused = all && (nsl > 0 || ntiles > 0) && env_int("KGE_REL_FUSED", 1) != 0;
   const bool rel_side = sd && !rel_fused && (!sch.rel_main || !all);
   RelArgs rl;
   rl.rel = m->relation_embedding; rl.R = m->nrelation; rl.E = m->nentity; rl.B = B; rl.Bn = B * n; rl.Lr = Lr;
@@ -334,14 +359,33 @@ int run_grad(const kge_model_desc* m, const Geom& geo, int mode, const int64_t* 
   ea.minw = ent_minw;
   ea.nsl = nsl;
   if (nsl > 0) {
-    static const int pf = env_int("KGE_ENT_PF", 6);  // 6: 4 rows in flight, Adam moments up front, packed RotatE math (measured best)
+    // 7: 4 rows in flight, Adam moments up front, packed RotatE math, non-temporal
+    // row/Adam/gradient stream (measured best: entity pass 0.29 → 0.24 ms; 6 = same with plain loads/stores)
+    static const int pf = env_int("KGE_ENT_PF", 7);
     ea.minw = pf;
   }
   ea.slice_w = nsl > 0 ? (geo.eg.S + nsl - 1) / nsl : 0;
   ea.adam = adam_t(adam ? &adam->entity : nullptr);
   ea.adamk = ak;
   ea.rel = rl;
-  ea.rel_blocks = rel_fused ? (m->nrelation + 3) / 4 : 0;
+  ea.B = B;
+  ea.ntiles = ntiles;
+  ea.ngroups = 0;
+  if (ntiles > 0) {  // about one workgroup per CU (each holds ~B*136 B of LDS)
+    const int cus = device_cus();
+    ea.ngroups = (cus + ntiles / 2) / ntiles;
+    if (ea.ngroups < 1) ea.ngroups = 1;
+  }
+  const int rows_per_rel_block = ntiles > 0 ? TL_THREADS / 64 : 4;
+  ea.rel_blocks = rel_fused ? (m->nrelation + rows_per_rel_block - 1) / rows_per_rel_block : 0;
+  ea.meta = w.meta;
+  if (ntiles > 0 && e_end > e_begin) {
+    MetaArgs ma;
+    ma.off = w.off; ma.occ = w.occ; ma.g = ea.g; ma.e_begin = e_begin; ma.e_end = e_end;
+    ma.Bn = B * n; ma.n = n; ma.N = B * n + 2 * B; ma.meta = w.meta;
+    st = launch_status(launch_occ_meta(ma, s));
+    if (st) return st;
+  }
   if (e_end > e_begin) {
     st = launch_status(op.entity(mode, geo.vec, geo.ns, ea, s));
     if (st) return st;

@@ -195,6 +195,20 @@ static inline unsigned grid_for(int64_t n, unsigned cap = 4096) {
 // Bucket offsets: a device-wide exclusive scan of cnt[0..nb] (cnt[nb] = 0, so
 // off[nb] = total) — rocPRIM's decoupled look-back scan, integer and exact;
 // its scratch comes from the caller's workspace.
+// One thread per CSR entry of the chunk's entity buckets.
+__global__ __launch_bounds__(256) void k_occ_meta(MetaArgs a) {
+  const int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int32_t lo = a.off[a.e_begin], hi = a.off[a.e_end];
+  if (c < lo || c >= hi) return;
+  const int32_t o = a.occ[c];
+  int2 m = make_int2(-1, 0);
+  if (o < a.Bn) {
+    m.x = (int32_t)((uint32_t)o / (uint32_t)a.n);
+    m.y = __float_as_int(a.g[o]);
+  }
+  a.meta[c] = m;
+}
+
 size_t csr_scan_temp_bytes(int64_t nb) {
   static thread_local int64_t last_nb = -1;  // the query is per size; remember the last one
   static thread_local size_t last_bytes = 0;
@@ -219,6 +233,12 @@ int launch_csr(const CsrArgs& a, hipStream_t s) {
   if (e != hipSuccess) return (int)e;
   hipLaunchKernelGGL(k_csr_fill, dim3(grid_for(N)), dim3(256), 0, s, a);
   hipLaunchKernelGGL(k_csr_rank, dim3(grid_for(N)), dim3(256), 0, s, a);
+  return (int)hipGetLastError();
+}
+
+int launch_occ_meta(const MetaArgs& a, hipStream_t s) {
+  if (a.N <= 0) return 0;
+  hipLaunchKernelGGL(k_occ_meta, dim3((unsigned)((a.N + 255) / 256)), dim3(256), 0, s, a);
   return (int)hipGetLastError();
 }
 

@@ -49,6 +49,7 @@ struct Consts {
 
 // ---------------------------------------------------------------- loads
 typedef float tf2 __attribute__((ext_vector_type(2)));  // a register pair (v_pk_*_f32 operand)
+typedef float tf4 __attribute__((ext_vector_type(4)));
 
 template <int VEC>
 __device__ __forceinline__ void ldv(const float* __restrict__ p, float (&x)[VEC]) {
@@ -178,6 +179,7 @@ __device__ __forceinline__ float wave_sum(float x) {
 // model.py:209) stays an IEEE division.
 __device__ __forceinline__ float fsqrt(float x) { return __builtin_amdgcn_sqrtf(x); }
 __device__ __forceinline__ float frcp(float x) { return __builtin_amdgcn_rcpf(x); }
+__device__ __forceinline__ float frsq(float x) { return __builtin_amdgcn_rsqf(x); }
 
 __device__ __forceinline__ float sgnf(float x) { return (x > 0.f) ? 1.f : ((x < 0.f) ? -1.f : 0.f); }
 
@@ -293,8 +295,8 @@ struct Elem {
       gqa = ea; gqb = eb; gea = qa; geb = qb;
     } else if constexpr (M == ROTATE) {
       const float dr = qa - ea, di = qb - eb;
-      const float rho = fsqrt(dr * dr + di * di);
-      const float inv = (rho > 0.f) ? frcp(rho) : 0.f;  // norm backward is masked at 0
+      const float s2 = dr * dr + di * di;
+      const float inv = (s2 > 0.f) ? frsq(s2) : 0.f;  // 1/|.|; norm backward is masked at 0
       const float ur = dr * inv, ui = di * inv;
       gqa = -ur; gqb = -ui; gea = ur; geb = ui;
     } else {

@@ -77,6 +77,12 @@ struct RelArgs {
   AdamK adamk;
 };
 
+// LDS-tiled entity pass (k_entity_tl): one column tile of q per workgroup
+constexpr int TL_COLS = 32;          // floats of one q row per tile (16 complex or 32 real dims)
+constexpr int TL_STRIDE = TL_COLS + 2;  // LDS row pitch in floats (136 B)
+constexpr int TL_THREADS = 1024;
+constexpr int TL_MAX_ROWS = 1152;    // batch rows that fit: 1152 * 136 B = 153 KiB of the 160 KiB LDS
+
 struct EntArgs {
   const float* ent;
   const float* modulus;
@@ -98,6 +104,9 @@ struct EntArgs {
   int write_grad;       // store grad_ent (unless the fused optimizer asks not to)
   int minw;             // k_entity: min waves/SIMD the register budget targets (3 or 4);
                         // k_entity_sl: q rows in flight per wave (4 or 8)
+  int ntiles, ngroups;  // > 0: LDS-tiled pass k_entity_tl (ntiles column tiles x ngroups entity ranges)
+  int64_t B;            // batch rows (the q buffer's height)
+  const int2* meta;     // k_entity_tl: per CSR entry (q row or -1, dL/ds bits), from k_occ_meta
   int nsl;              // > 0: column-sliced pass k_entity_sl with nsl slices of slice_w slots (VEC = 4)
   int slice_w;
   AdamT adam;           // fused optimizer step (adam.p == null: none)

@@ -435,20 +435,26 @@ def test_config2_full_size_properties():
     assert ((acc - full).abs() <= tol).all()
 
 
-@pytest.mark.parametrize("name", ["RotatE", "ComplEx", "TransE", "pRotatE"])
-def test_entity_pass_column_slices_bitwise(name, monkeypatch):
-    """The column-sliced entity pass (k_entity_sl, nsl = 1, 2, 4, 8 slices) and
-    the row-per-wave pass (KGE_ENT_SLICES=0) apply the same per-element
-    arithmetic in the same occurrence order: identical gradients and fused
-    Adam updates, bit for bit (the regulariser's partial sums only regroup)."""
-    E, R, d, B, n = 300, 7, 200, 24, 40   # 50 slots per (half) row: 1..8 slices all fit
+@pytest.mark.parametrize("name,d,B", [("RotatE", 200, 24), ("ComplEx", 200, 24), ("TransE", 200, 24),
+                                      ("pRotatE", 200, 24), ("DistMult", 200, 24), ("RotatE", 104, 1100),
+                                      ("DistMult", 52, 700)])
+def test_entity_pass_column_slices_bitwise(name, d, B, monkeypatch):
+    """The LDS-tiled entity pass (k_entity_tl, KGE_ENT_TILE=1), the column-sliced
+    pass (k_entity_sl, nsl = 1, 2, 4, 8 slices; the default) and the row-per-wave pass
+    (KGE_ENT_TILE=0 KGE_ENT_SLICES=0) apply the same per-element arithmetic in
+    the same occurrence order: identical gradients and fused Adam updates, bit
+    for bit (the regulariser's partial sums only regroup).  d = 200 / 104 / 52
+    leave the last 16-column tile partial; B = 1100 fills most of the LDS."""
+    E, R, n = 300, 7, 40   # d = 200: 50 slots per (half) row: 1..8 slices all fit
     args = Namespace(negative_adversarial_sampling=True, adversarial_temperature=1.0, uni_weight=False,
-                     regularization=1e-4 if name == "ComplEx" else 0.0)
+                     regularization=1e-4 if name in ("ComplEx", "DistMult") else 0.0)
     pos, neg, w = synth.kge_batch(88, B, n, E, R)
     P, N, W = torch.from_numpy(pos).to(DEV), torch.from_numpy(neg).to(DEV), torch.from_numpy(w).to(DEV)
     out = {}
-    for nsl in ("0", "1", "2", "4", "8"):
-        monkeypatch.setenv("KGE_ENT_SLICES", nsl)
+    variants = ("0", "1", "2", "4", "8", "tile") if d == 200 else ("0", "tile")
+    for nsl in variants:
+        monkeypatch.setenv("KGE_ENT_TILE", "1" if nsl == "tile" else "0")
+        monkeypatch.setenv("KGE_ENT_SLICES", "0" if nsl == "tile" else nsl)
         m, *_ = build_model(name, E, R, d, 12.0, 5)
         opt = KGEAdam([p for p in m.parameters() if p.requires_grad], lr=1e-3)
         res = []
@@ -458,7 +464,7 @@ def test_entity_pass_column_slices_bitwise(name, monkeypatch):
             res.append((losses.cpu().clone(), m.entity_embedding.grad.cpu().clone(),
                         m.entity_embedding.detach().cpu().clone()))
         out[nsl] = res
-    for nsl in ("1", "2", "4", "8"):
+    for nsl in variants[1:]:
         for (l0, g0, p0), (l1, g1, p1) in zip(out["0"], out[nsl]):
             assert torch.equal(g0, g1) and torch.equal(p0, p1), nsl
             torch.testing.assert_close(l0[:4], l1[:4], rtol=1e-6, atol=0)
