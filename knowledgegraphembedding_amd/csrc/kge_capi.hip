@@ -431,7 +431,7 @@ RowArgs row_args(const kge_model_desc* m, const Geom& geo, const int64_t* pos, c
   }();
   ra.pipe = pipe;
   ra.fuse_q = env_int("KGE_FUSE_Q", 1);  // measured +1.8 %; bit-identical to the separate k_build_q
-  ra.fuse_epi = env_int("KGE_FUSE_EPI", 0);  // measured −1 %: the epilogue pushes k_row to 23 spilled VGPRs
+  ra.fuse_epi = env_int("KGE_FUSE_EPI", 1);  // measured +1 % once k_row's RotatE math went to register pairs (no spills)
   return ra;
 }
 

@@ -152,6 +152,35 @@ __device__ __forceinline__ void zero_row(Row<NS, VEC, CPLX>& r) {
 // row loads use the scalar-base + 32-bit-lane-offset form.
 __device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
 
+// Buffer descriptors (wave-uniform base and size): lanes with nothing to do
+// pass an out-of-range offset, so loads return 0 and stores are dropped by
+// the hardware range check — no exec branches around memory operations,
+// which keeps the vmcnt bookkeeping static across the software pipeline.
+constexpr uint32_t BUF_OOB = 0x7FFFFFF0u;
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* base, uint64_t bytes) {
+  const uint64_t b = (uint64_t)base;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)b);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(b >> 32));
+  const uint32_t n = __builtin_amdgcn_readfirstlane((uint32_t)bytes);
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), (short)0, (int)n, 0x00020000);
+}
+// (the b32 builtins move raw 32-bit words: reinterpret, never convert)
+__device__ __forceinline__ float buf_ld(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));
+}
+__device__ __forceinline__ int32_t buf_ldi(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  return (int32_t)__builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0);
+}
+__device__ __forceinline__ void buf_st(__amdgpu_buffer_rsrc_t r, uint32_t off, float v) {
+  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, off, 0, 0);
+}
+
+__device__ __forceinline__ void buf_ld4(__amdgpu_buffer_rsrc_t r, uint32_t off, float (&x)[4]) {
+  typedef unsigned int u4 __attribute__((ext_vector_type(4)));
+  const u4 v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
+  x[0] = __uint_as_float(v.x); x[1] = __uint_as_float(v.y); x[2] = __uint_as_float(v.z); x[3] = __uint_as_float(v.w);
+}
+
 // ------------------------------------------------------------ reductions
 template <int CTRL>
 __device__ __forceinline__ float dppf(float v) {
