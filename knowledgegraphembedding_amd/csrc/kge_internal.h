@@ -62,6 +62,10 @@ struct RowArgs {
   void (*timer_mid)(hipStream_t);  // stage-timer hook between the row-pass launches (or null)
 };
 
+// k_row's LDS merge buffer: [2][Le] floats, and at least the 256 floats the
+// fused Σw reduction (block_weight_sum) uses as its tree
+__host__ __device__ inline int vb_floats(int Le) { return 2 * Le > 256 ? 2 * Le : 256; }
+
 struct RelArgs {
   const float* rel;
   int64_t R, E, B, Bn;

@@ -470,13 +470,17 @@ def test_entity_pass_column_slices_bitwise(name, d, B, monkeypatch):
             torch.testing.assert_close(l0[:4], l1[:4], rtol=1e-6, atol=0)
 
 
-@pytest.mark.parametrize("name", NAMES)
-def test_fused_q_build_bitwise(name, monkeypatch):
+@pytest.mark.parametrize("name,E,d,B,n", [(nm, 400, 120, 24, 40) for nm in NAMES] +
+                         [("RotatE", 300, 64, 8, 32), ("RotatE", 2000, 100, 64, 32), ("DistMult", 500, 16, 300, 8)])
+def test_fused_q_build_bitwise(name, E, d, B, n, monkeypatch):
     """k_row building q and Σw in its own prologue (KGE_FUSE_Q=1), and also
     running the epilogue in its tail (KGE_FUSE_EPI=1), give the separate
     launches' losses and gradients bit for bit (same per-element arithmetic,
-    same fixed-order Σw reduction, same epilogue function)."""
-    E, R, d, B, n = 400, 9, 120, 24, 40
+    same fixed-order Σw reduction, same epilogue function).  Many blocks per
+    launch (B = 64, 300) exercise the fused tail's c_i, which must not read the
+    Σw that block 0 publishes in the same launch; d = 16 with B = 300 needs the
+    Σw tree's 256 floats of LDS beyond the 2·Le merge buffer."""
+    R = 9
     pos, neg, w = synth.kge_batch(91, B, n, E, R)
     P, N, W = torch.from_numpy(pos).to(DEV), torch.from_numpy(neg).to(DEV), torch.from_numpy(w).to(DEV)
     res = {}
