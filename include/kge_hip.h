@@ -197,6 +197,41 @@ int kge_train_step(const kge_model_desc *m, int32_t mode, const int64_t *pos, co
                    int32_t *err_flag, void *stream);
 
 /*
+ * Data-parallel FACTOR EXCHANGE (distributed.py, exchange "factors"): instead
+ * of all-reducing the dense [E, entity_dim] gradient, the ranks all-gather the
+ * row pass's per-row factors — dL/ds [B, nneg], dL/dq [B, entity_dim] and the
+ * row statistics [B, 4] — and every rank runs the rest of the step for the
+ * GLOBAL batch itself.  On point-to-point xGMI with few ranks this moves
+ * ~9 MB per rank instead of ~2·(N-1)/N · 120 MB (RotatE FB15k).
+ *
+ * kge_train_rows_slice: the negative-row pass (q build + k_row, no epilogue)
+ * for `nrows` rows; pos/neg/subsampling_weight point at the slice's own rows,
+ * weight_sum at the GLOBAL Σw (kge_weight_sum over all weights: the same
+ * fixed order as a single process's in-kernel sum), uni_batch = global batch.
+ * Writes g_out [nrows, nneg], dq_out [nrows, entity_dim] and columns 1-2 of
+ * stats_out [nrows, 4] (pass the slice's place in the gathered buffers).
+ * Workspace: kge_train_workspace_bytes(m, nrows, nneg).
+ *
+ * kge_train_step_from_rows: the rest of a kge_train_step (adam != NULL) or
+ * kge_train_step_grads (adam == NULL) for the global batch from the gathered
+ * buffers: q rebuilt, positive scores and chain rule, occurrence CSR, entity-
+ * major and relation passes, losses.  Bit-identical to the single-process call
+ * on the whole batch.  Workspace: kge_train_workspace_bytes(m, batch, nneg).
+ */
+int kge_train_rows_slice(const kge_model_desc *m, int32_t mode, const int64_t *pos, const int64_t *neg,
+                         int64_t nrows, int64_t nneg, const float *subsampling_weight, const float *weight_sum,
+                         int32_t uni_weight, int64_t uni_batch, int32_t adversarial, float adversarial_temperature,
+                         float *g_out, float *dq_out, float *stats_out, void *workspace, size_t workspace_bytes,
+                         int32_t *err_flag, void *stream);
+int kge_train_step_from_rows(const kge_model_desc *m, int32_t mode, const int64_t *pos, const int64_t *neg,
+                             int64_t batch, int64_t nneg, const float *subsampling_weight, const float *weight_sum,
+                             int32_t uni_weight, int64_t uni_batch, float regularization, const float *g_in,
+                             const float *dq_in, float *stats_inout, const kge_adam_desc *adam,
+                             float *grad_entity, float *grad_relation, float *grad_modulus, float *losses_out,
+                             void *workspace, size_t workspace_bytes, int32_t *err_flag, void *stream);
+
+
+/*
  * Σ subsampling_weight into *out (device scalar) — the denominator of
  * model.py:285-286; exposed so data-parallel ranks can all-reduce it.
  */

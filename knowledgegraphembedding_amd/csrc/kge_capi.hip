@@ -220,12 +220,16 @@ Side* side_for_device() {
   return &sd;
 }
 
+// Data-parallel factor exchange (kge_train_rows_slice / kge_train_step_from_rows)
+enum XStage : int { XS_NONE = 0, XS_ROWS_ONLY = 1, XS_FROM_ROWS = 2 };
+
 // Shared body of backward and train.  Caller's stream: q build → gather loop →
 // epilogue → entity pass → finalise; side stream: CSR ∥ row pass, relation pass ∥ entity pass.
 int run_grad(const kge_model_desc* m, const Geom& geo, int mode, const int64_t* pos, const int64_t* neg,
              int64_t neg_stride, int64_t B, int64_t n, RowArgs ra, GradWs w, float* grad_entity,
              float* grad_relation, float* grad_modulus, float reg, FinArgs fa, const kge_adam_desc* adam,
-             int32_t* err, hipStream_t s, int phases = KGE_PHASE_ALL, int64_t e_begin = 0, int64_t e_end = -1) {
+             int32_t* err, hipStream_t s, int phases = KGE_PHASE_ALL, int64_t e_begin = 0, int64_t e_end = -1,
+             int xstage = XS_NONE) {
   const ModelOps& op = ops_for(m->model);
   AdamK ak;
   ak.b1 = adam ? adam->beta1 : 0.f;
@@ -250,7 +254,7 @@ int run_grad(const kge_model_desc* m, const Geom& geo, int mode, const int64_t* 
   // stage timing: a full call records all 7 marks; a phased ROWS call (the
   // data-parallel path) records the row-pass marks and pads the rest, so the
   // row pass is timed live on every rank either way
-  const bool timed = (phases & KGE_PHASE_ROWS) && g_timer.on && ra.op == ROW_TRAIN &&
+  const bool timed = (phases & KGE_PHASE_ROWS) && xstage != XS_FROM_ROWS && g_timer.on && ra.op == ROW_TRAIN &&
                      (g_timer.seen++ % (size_t)g_timer.period) == 0;
   ra.timer_mid = timed ? &timer_mark : nullptr;
   Side* sd = side_for_device();
@@ -296,6 +300,19 @@ int run_grad(const kge_model_desc* m, const Geom& geo, int mode, const int64_t* 
   rl.adam = adam_t(adam ? &adam->relation : nullptr);
   rl.adamk = ak;
 
+  if (xstage == XS_ROWS_ONLY) {
+    // the negative-row pass alone (q build + k_row), dL/dq to global memory for
+    // the exchange; no epilogue, CSR or relation pass (kge_train_rows_slice)
+    ra.fuse_epi = 0;
+    if (timed) g_timer.mark(s);
+    st = launch_status(op.row(mode, geo.vec, geo.ns, 0, ra, lds, s));
+    if (st) return st;
+    if (timed)
+      for (int k = 0; k < 5; ++k) g_timer.mark(s);  // row-pass end + the stages not in this call
+    return KGE_OK;
+  }
+  if (xstage == XS_FROM_ROWS) ra.fuse_epi = 0;  // the epilogue reads the gathered dL/dq (k_row_epi)
+
   if (phases & KGE_PHASE_ROWS) {
   // fork point: the occurrence CSR needs only the batch indices (recorded
   // before anything else is queued, so the side stream never waits for the
@@ -305,7 +322,8 @@ int run_grad(const kge_model_desc* m, const Geom& geo, int mode, const int64_t* 
   // q build + gather loop on the caller's stream, launched first so the GPU
   // is on the long kernel while the host queues everything else
   if (timed) g_timer.mark(s);
-  st = launch_status(op.row(mode, geo.vec, geo.ns, 0, ra, lds, s));
+  // (XS_FROM_ROWS: the row pass ran on the ranks; only q is rebuilt here)
+  st = launch_status(op.row(mode, geo.vec, geo.ns, xstage == XS_FROM_ROWS ? 2 : 0, ra, lds, s));
   if (st) return st;
   if (timed) g_timer.mark(s);
 
@@ -543,13 +561,16 @@ static int train_impl(const kge_model_desc* m, int32_t mode, const int64_t* pos,
                       int64_t uni_batch, int32_t adversarial, float adversarial_temperature, float regularization,
                       const kge_adam_desc* adam, float* grad_entity, float* grad_relation, float* grad_modulus,
                       float* losses_out, void* workspace, size_t workspace_bytes, int32_t* err_flag, void* stream,
-                      int32_t phases = KGE_PHASE_ALL, int64_t e_begin = 0, int64_t e_end = -1) {
+                      int32_t phases = KGE_PHASE_ALL, int64_t e_begin = 0, int64_t e_end = -1, int xstage = XS_NONE,
+                      float* rows_g = nullptr, float* rows_dq = nullptr, float* rows_stats = nullptr) {
   Geom geo;
   int st = check_model(m, &geo);
   if (st) return st;
   if (mode != KGE_HEAD_BATCH && mode != KGE_TAIL_BATCH) return KGE_ERR_MODE;
-  if (!pos || !neg || !grad_entity || !grad_relation || !err_flag || !losses_out || batch < 1 || nneg < 1)
-    return KGE_ERR_ARG;
+  if (xstage == XS_NONE && (!grad_entity || !grad_relation || !losses_out)) return KGE_ERR_ARG;
+  if (xstage != XS_NONE && (!rows_g || !rows_dq || !rows_stats)) return KGE_ERR_ARG;
+  if (xstage == XS_FROM_ROWS && (!grad_entity || !grad_relation || !losses_out)) return KGE_ERR_ARG;
+  if (!pos || !neg || !err_flag || batch < 1 || nneg < 1) return KGE_ERR_ARG;
   if (adam) {
     if (!adam->entity.param || !adam->entity.exp_avg || !adam->entity.exp_avg_sq || !adam->relation.param ||
         !adam->relation.exp_avg || !adam->relation.exp_avg_sq)
@@ -559,10 +580,16 @@ static int train_impl(const kge_model_desc* m, int32_t mode, const int64_t* pos,
     if (m->model == KGE_PROTATE && adam->modulus.param && adam->modulus.param != m->modulus) return KGE_ERR_ARG;
   }
   if (!uni_weight && !subsampling_weight) return KGE_ERR_ARG;
-  if (m->model == KGE_PROTATE && !grad_modulus) return KGE_ERR_ARG;
+  if (m->model == KGE_PROTATE && !grad_modulus && xstage != XS_ROWS_ONLY) return KGE_ERR_ARG;
+  if (xstage != XS_NONE && !uni_weight && !weight_sum) return KGE_ERR_ARG;  // the global Σw comes from the caller
   size_t need = 0;
   GradWs w = carve_grad(workspace, m, batch, nneg, &need);
   if (!workspace || workspace_bytes < need) return KGE_ERR_WORKSPACE;
+  if (xstage != XS_NONE) {  // the exchanged per-row factors live in the caller's (gathered) buffers
+    w.g = rows_g;
+    w.dq = rows_dq;
+    w.row_stats = rows_stats;
+  }
   hipStream_t s = as_stream(stream);
   const float* wsum = weight_sum;
   float* wsum_out = nullptr;
@@ -596,7 +623,29 @@ static int train_impl(const kge_model_desc* m, int32_t mode, const int64_t* pos,
   if (e_begin < 0 || e_begin > e_end || e_end > m->nentity) return KGE_ERR_ARG;
   return run_grad(m, geo, mode, pos, neg, nneg, batch, nneg, ra, w, grad_entity, grad_relation,
                   m->model == KGE_PROTATE ? grad_modulus : nullptr, regularization, fa, adam, err_flag, s, phases,
-                  e_begin, e_end);
+                  e_begin, e_end, xstage);
+}
+
+int kge_train_rows_slice(const kge_model_desc* m, int32_t mode, const int64_t* pos, const int64_t* neg,
+                         int64_t nrows, int64_t nneg, const float* subsampling_weight, const float* weight_sum,
+                         int32_t uni_weight, int64_t uni_batch, int32_t adversarial, float adversarial_temperature,
+                         float* g_out, float* dq_out, float* stats_out, void* workspace, size_t workspace_bytes,
+                         int32_t* err_flag, void* stream) {
+  return train_impl(m, mode, pos, neg, nrows, nneg, subsampling_weight, weight_sum, uni_weight, uni_batch, adversarial,
+                    adversarial_temperature, 0.f, nullptr, nullptr, nullptr, nullptr, nullptr, workspace,
+                    workspace_bytes, err_flag, stream, KGE_PHASE_ROWS, 0, -1, XS_ROWS_ONLY, g_out, dq_out, stats_out);
+}
+
+int kge_train_step_from_rows(const kge_model_desc* m, int32_t mode, const int64_t* pos, const int64_t* neg,
+                             int64_t batch, int64_t nneg, const float* subsampling_weight, const float* weight_sum,
+                             int32_t uni_weight, int64_t uni_batch, float regularization, const float* g_in,
+                             const float* dq_in, float* stats_inout, const kge_adam_desc* adam, float* grad_entity,
+                             float* grad_relation, float* grad_modulus, float* losses_out, void* workspace,
+                             size_t workspace_bytes, int32_t* err_flag, void* stream) {
+  return train_impl(m, mode, pos, neg, batch, nneg, subsampling_weight, weight_sum, uni_weight, uni_batch, 1, 1.f,
+                    regularization, adam, grad_entity, grad_relation, grad_modulus, losses_out, workspace,
+                    workspace_bytes, err_flag, stream, KGE_PHASE_ALL, 0, -1, XS_FROM_ROWS, const_cast<float*>(g_in),
+                    const_cast<float*>(dq_in), stats_inout);
 }
 
 int kge_train_step_grads_phased(const kge_model_desc* m, int32_t mode, const int64_t* pos, const int64_t* neg,

@@ -145,18 +145,13 @@ __global__ __launch_bounds__(1024) void k_finalize(FinArgs a) {
   }
 }
 
-__global__ __launch_bounds__(1024) void k_weight_sum(const float* __restrict__ w, int64_t n, float* out) {
-  __shared__ float red[1024];
-  const int tid = threadIdx.x;
-  float s = 0.f;
-  for (int64_t i = tid; i < n; i += 1024) s += w[i];
-  red[tid] = s;
-  __syncthreads();
-  for (int o = 512; o > 0; o >>= 1) {
-    if (tid < o) red[tid] += red[tid + o];
-    __syncthreads();
-  }
-  if (tid == 0) out[0] = red[0];
+// Same fixed order as k_row's / k_build_q's in-kernel Σw (block_weight_sum,
+// 256 threads), so a Σw computed here is bit-identical to the one a single
+// process computes for the same weights (the data-parallel factor exchange).
+__global__ __launch_bounds__(256) void k_weight_sum(const float* __restrict__ w, int64_t n, float* out) {
+  __shared__ float red[256];
+  const float tot = block_weight_sum(w, n, red);
+  if (threadIdx.x == 0) out[0] = tot;
 }
 
 // ------------------------------------------------------------------ Adam
@@ -253,7 +248,7 @@ int launch_finalize(const FinArgs& a, hipStream_t s) {
 }
 
 int launch_weight_sum(const float* w, int64_t n, float* out, hipStream_t s) {
-  hipLaunchKernelGGL(k_weight_sum, dim3(1), dim3(1024), 0, s, w, n, out);
+  hipLaunchKernelGGL(k_weight_sum, dim3(1), dim3(256), 0, s, w, n, out);
   return (int)hipGetLastError();
 }
 

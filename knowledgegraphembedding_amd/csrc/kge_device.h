@@ -181,6 +181,23 @@ __device__ __forceinline__ void buf_ld4(__amdgpu_buffer_rsrc_t r, uint32_t off, 
   x[0] = __uint_as_float(v.x); x[1] = __uint_as_float(v.y); x[2] = __uint_as_float(v.z); x[3] = __uint_as_float(v.w);
 }
 
+// Σ subsampling_weight (model.py:285-286) by one 256-thread block in a fixed
+// order (strided partial sums, then a tree in `red`); every caller gets the
+// same bits.  Returns the sum in every thread.
+__device__ __forceinline__ float block_weight_sum(const float* __restrict__ w, int64_t B, float* red) {
+  float s = 0.f;
+  for (int64_t k = threadIdx.x; k < B; k += 256) s += w[k];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  const float tot = red[0];
+  __syncthreads();
+  return tot;
+}
+
 // ------------------------------------------------------------ reductions
 template <int CTRL>
 __device__ __forceinline__ float dppf(float v) {

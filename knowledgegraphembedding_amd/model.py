@@ -410,9 +410,14 @@ class KGEModel(nn.Module):
             # row-partitioned entity table (partition.py): reduce-scatter to the owners
             losses = part.train_grads(model, positive_sample, negative_sample, subsampling_weight, mode, args)
         elif dp is not None:
-            from .distributed import dp_train_grads
-            losses = dp_train_grads(model, positive_sample, negative_sample, subsampling_weight, mode, args,
-                                    optimizer=optimizer)
+            import torch.distributed as dist
+            from .distributed import dp_exchange_mode, dp_train_grads, dp_train_step_factors
+            if dp_exchange_mode(dist.get_world_size(dp), getattr(args, 'dp_exchange', None)) == "factors":
+                losses = dp_train_step_factors(model, positive_sample, negative_sample, subsampling_weight, mode,
+                                               args, optimizer=optimizer)
+            else:
+                losses = dp_train_grads(model, positive_sample, negative_sample, subsampling_weight, mode, args,
+                                        optimizer=optimizer)
         else:
             # a KGEAdam optimizer is stepped inside the gradient passes; any
             # other optimizer sees ordinary dense .grad tensors.  The loss

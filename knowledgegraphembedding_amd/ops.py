@@ -211,6 +211,59 @@ def train_step_grads(desc: _lib.ModelDesc, mode: str, pos: torch.Tensor, neg: to
         _lib.check(lib.kge_train_step(*common, adam, *tail), "kge_train_step")
 
 
+def _train_ws(desc: _lib.ModelDesc, B: int, n: int, dev) -> torch.Tensor:
+    lib = _lib.load()
+    key = (desc.entity_dim, desc.relation_dim, desc.nentity, desc.nrelation, B, n)
+    need = _WS_BYTES.get(key)
+    if need is None:
+        need = _WS_BYTES[key] = lib.kge_train_workspace_bytes(desc, B, n)
+    return state(dev).workspace(need)
+
+
+def train_rows_slice(desc: _lib.ModelDesc, mode: str, pos: torch.Tensor, neg: torch.Tensor, sub_w: torch.Tensor,
+                     weight_sum_dev: Optional[torch.Tensor], dev, *, adversarial: bool, temperature: float,
+                     uni_weight: bool, uni_batch: int, g_out: torch.Tensor, dq_out: torch.Tensor,
+                     stats_out: torch.Tensor) -> None:
+    """The negative-row pass alone for this rank's rows (kge_train_rows_slice):
+    dL/ds, dL/dq and the row statistics into the rank's place in the gather
+    buffers (the data-parallel factor exchange, distributed.py)."""
+    if mode not in ("head-batch", "tail-batch"):
+        raise ValueError("Training batch mode %s not supported" % mode)
+    pos, neg = _idx(pos, dev), _idx(neg, dev)
+    w = sub_w.to(dev, dtype=torch.float32).contiguous().view(-1)
+    B, n = neg.shape
+    for t, shape in ((g_out, (B, n)), (dq_out, (B, desc.entity_dim)), (stats_out, (B, 4))):
+        if tuple(t.shape) != shape or not t.is_contiguous() or t.dtype != torch.float32:
+            raise ValueError(f"row buffer of shape {tuple(t.shape)}, expected contiguous fp32 {shape}")
+    ws = _train_ws(desc, B, n, dev)
+    st = state(dev)
+    _lib.check(_lib.load().kge_train_rows_slice(
+        desc, _lib.MODE_IDS[mode], pos.data_ptr(), neg.data_ptr(), B, n, w.data_ptr(), _ptr(weight_sum_dev),
+        int(bool(uni_weight)), int(uni_batch), int(bool(adversarial)), float(temperature), g_out.data_ptr(),
+        dq_out.data_ptr(), stats_out.data_ptr(), ws.data_ptr(), ws.numel(), st.err.data_ptr(), _stream(dev)),
+        "kge_train_rows_slice")
+
+
+def train_step_from_rows(desc: _lib.ModelDesc, mode: str, pos: torch.Tensor, neg: torch.Tensor, sub_w: torch.Tensor,
+                         weight_sum_dev: Optional[torch.Tensor], dev, *, uni_weight: bool, uni_batch: int,
+                         regularization: float, g_in: torch.Tensor, dq_in: torch.Tensor, stats: torch.Tensor,
+                         grad_entity: torch.Tensor, grad_relation: torch.Tensor, grad_modulus: Optional[torch.Tensor],
+                         losses: torch.Tensor, adam: Optional[_lib.AdamDesc] = None) -> None:
+    """The rest of the step for the whole (gathered) batch from the exchanged
+    row factors (kge_train_step_from_rows); bit-identical to one process
+    running train_step_grads / the fused step on that batch."""
+    pos, neg = _idx(pos, dev), _idx(neg, dev)
+    w = sub_w.to(dev, dtype=torch.float32).contiguous().view(-1)
+    B, n = neg.shape
+    ws = _train_ws(desc, B, n, dev)
+    st = state(dev)
+    _lib.check(_lib.load().kge_train_step_from_rows(
+        desc, _lib.MODE_IDS[mode], pos.data_ptr(), neg.data_ptr(), B, n, w.data_ptr(), _ptr(weight_sum_dev),
+        int(bool(uni_weight)), int(uni_batch), float(regularization), g_in.data_ptr(), dq_in.data_ptr(),
+        stats.data_ptr(), adam, grad_entity.data_ptr(), grad_relation.data_ptr(), _ptr(grad_modulus),
+        losses.data_ptr(), ws.data_ptr(), ws.numel(), st.err.data_ptr(), _stream(dev)), "kge_train_step_from_rows")
+
+
 def adam_step(param: torch.Tensor, grad: torch.Tensor, exp_avg: torch.Tensor, exp_avg_sq: torch.Tensor, *,
               step: int, lr: float, beta1: float, beta2: float, eps: float) -> None:
     """torch.optim.Adam's update for one tensor (bias corrections in double, like torch)."""

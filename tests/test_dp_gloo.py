@@ -119,3 +119,73 @@ def test_dp_two_ranks_match_global_batch(name, adv, uni, reg):
         np.testing.assert_allclose(g_r, gr.numpy(), rtol=1e-4, atol=1e-6 * np.abs(gr.numpy()).max())
         if name == "pRotatE":
             np.testing.assert_allclose(out[rank][3], gm.numpy(), rtol=1e-4)
+
+
+# ---------------------------------------------------------------- factor exchange
+# The exchange's data movement (distributed.dp_train_step_factors) with world
+# size 2 over gloo on CPU.  The two HIP entry points are replaced by stand-ins
+# that write a known function of the rank's own rows and record what the
+# global step receives (test infrastructure); the parity of the real kernels
+# is tests/test_dp_factors_gpu.py (bit-identical to one process).
+LE = 2 * D
+
+
+def _fx_rows(pos, neg, w, g_out, dq_out, stats_out):
+    g_out.copy_(neg.float() * w[:, None])
+    dq_out.copy_(pos.float().sum(1, keepdim=True) + torch.arange(LE, dtype=torch.float32))
+    stats_out.zero_()
+    stats_out[:, 1] = 2 * w
+    stats_out[:, 2] = 3 * w
+
+
+def _fx_worker(rank, world, port, uni, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from knowledgegraphembedding_amd import ops
+    seen = {}
+
+    def rows_slice(desc, mode, pos, neg, w, wsum, dev, *, adversarial, temperature, uni_weight, uni_batch, g_out,
+                   dq_out, stats_out):
+        seen["slice"] = (uni_batch, None if wsum is None else float(wsum[0]))
+        _fx_rows(pos, neg, w, g_out, dq_out, stats_out)
+
+    def from_rows(desc, mode, pos, neg, w, wsum, dev, *, uni_weight, uni_batch, regularization, g_in, dq_in, stats,
+                  grad_entity, grad_relation, grad_modulus, losses, adam=None):
+        seen["global"] = [t.clone() for t in (pos, neg, w, g_in, dq_in, stats)]
+        seen["global_scalars"] = (uni_batch, regularization, None if wsum is None else float(wsum[0]))
+        losses.copy_(torch.tensor([float(w.sum()), float(g_in.sum()), float(dq_in.sum()), float(stats.sum()), 0.]))
+
+    ops.train_rows_slice, ops.train_step_from_rows = rows_slice, from_rows
+    ops.weight_sum = lambda w, o: o.copy_(w.sum().reshape(1))
+    model = _make_model("RotatE")
+    pos, neg, w = synth.kge_batch(5, B, N, E, R)
+    sl = slice(rank * B // world, (rank + 1) * B // world)
+    args = Namespace(negative_adversarial_sampling=True, adversarial_temperature=1.0, uni_weight=uni,
+                     regularization=1e-3, dp_group=dist.group.WORLD)
+    losses = kdist.dp_train_step_factors(model, torch.from_numpy(pos[sl]), torch.from_numpy(neg[sl]),
+                                         torch.from_numpy(w[sl]), "tail-batch", args)
+    out[rank] = {"losses": losses.clone(), "seen": seen}
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("uni", [False, True])
+def test_factor_exchange_gathers_global_batch(uni):
+    world = 2
+    out = mp.Manager().dict()
+    mp.spawn(_fx_worker, args=(world, _free_port(), uni, out), nprocs=world, join=True)
+    pos, neg, w = (torch.from_numpy(x) for x in synth.kge_batch(5, B, N, E, R))
+    g = torch.empty(B, N)
+    dq = torch.empty(B, LE)
+    st = torch.empty(B, 4)
+    _fx_rows(pos, neg, w, g, dq, st)  # the stand-in over the whole batch = the two slices concatenated
+    assert kdist.dp_exchange_mode(2) == "factors" and kdist.dp_exchange_mode(8) == "grads"
+    for rank in range(world):
+        s = out[rank]["seen"]
+        for got, want in zip(s["global"], (pos, neg, w, g, dq, st)):
+            assert torch.equal(got, want.to(got.dtype))
+        assert s["slice"][0] == B and s["global_scalars"][:2] == (B, 1e-3)
+        if uni:
+            assert s["slice"][1] is None and s["global_scalars"][2] is None
+        else:  # Σw of the GLOBAL weights, on both sides of the exchange
+            assert s["slice"][1] == pytest.approx(float(w.sum())) and s["global_scalars"][2] == s["slice"][1]
+    assert torch.equal(out[0]["losses"], out[1]["losses"])
