@@ -38,6 +38,7 @@ import torch.distributed as dist
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 from knowledgegraphembedding_amd import KGEAdam, KGEModel, _lib  # noqa: E402
+from knowledgegraphembedding_amd.distributed import dp_exchange_mode  # noqa: E402
 
 E, R, D, B, NNEG, GAMMA, TEMP = 14951, 1345, 1000, 1024, 256, 24.0, 1.0
 METRIC = "scored (pos+neg) triples/sec, RotatE FB15k d=1000 b=1024 n=256, 1/2/4/8 GPU"
@@ -239,7 +240,8 @@ def main():
         "dtype": "fp32",
         "data": "synthetic (uniform ids, U(-range,range) tables), batches pre-staged in HBM",
         "variant": {"fused_adam": model.fuse_optimizer, "keep_grads": model.keep_grads,
-                    "row_pipe": os.environ.get("KGE_ROW_PIPE", "0"), "batches": sampler},
+                    "row_pipe": os.environ.get("KGE_ROW_PIPE", "0"), "batches": sampler,
+                    "dp_exchange": (None if group is None or part is not None else dp_exchange_mode(world))},
         "config": {"workload": wl["name"],
                    "entities": E, "relations": R, "hidden_dim": D, "batch_per_gpu": B, "global_batch": B * world,
                    "negatives": NNEG, "adversarial_temperature": TEMP, "gamma": GAMMA,

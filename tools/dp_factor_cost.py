@@ -1,0 +1,91 @@
+#!/usr/bin/env python3
+"""Compute side of the data-parallel factor exchange on one GPU (RotatE FB15k
+shape): the per-rank row pass on 1024 rows (kge_train_rows_slice) and the
+global step (kge_train_step_from_rows, fused Adam) on N·1024 gathered rows,
+for N = 1, 2, 4, 8 — against the single-device fused step.  Prints one JSON
+line; the exchange itself moves (B·Le + B·n + 4B)·4 + B·(n+3)·8 bytes per rank.
+
+    python tools/dp_factor_cost.py [--reps 30]
+"""
+import argparse
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from argparse import Namespace  # noqa: E402
+
+from knowledgegraphembedding_amd import KGEAdam, KGEModel, ops, synth  # noqa: E402
+
+E, R, D, B, N = 14951, 1345, 1000, 1024, 256
+
+
+def timed(fn, reps):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(reps):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / reps
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reps", type=int, default=30)
+    a = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(0)
+    m = KGEModel("RotatE", E, R, D, 24.0, True, False).to(dev)
+    opt = KGEAdam([p for p in m.parameters() if p.requires_grad], lr=1e-4)
+    args = Namespace(negative_adversarial_sampling=True, adversarial_temperature=1.0, uni_weight=False,
+                     regularization=0.0)
+    desc = m.desc()
+    Le = m.entity_dim
+    res = {"workload": "RotatE FB15k shape d=1000 b=1024/rank n=256", "reps": a.reps}
+    pos, neg, w = (torch.from_numpy(x).to(dev) for x in synth.kge_batch(9, B, N, E, R))
+
+    def single():
+        m.compute_train_grads(pos, neg, w, "tail-batch", args, optimizer=opt)
+        opt.step()
+    res["single_step_ms"] = timed(single, a.reps)
+
+    for world in (1, 2, 4, 8):
+        Bg = B * world
+        pg, ng, wg = (torch.from_numpy(x).to(dev) for x in synth.kge_batch(10 + world, Bg, N, E, R))
+        wsum = torch.empty(1, device=dev)
+        g_g, dq_g, st_g = torch.empty(Bg, N, device=dev), torch.empty(Bg, Le, device=dev), torch.empty(Bg, 4, device=dev)
+        ge, gr, gm, losses = m._grad_buffers()
+
+        def rows():
+            ops.weight_sum(wg, wsum)
+            ops.train_rows_slice(desc, "tail-batch", pg[:B], ng[:B], wg[:B], wsum, dev, adversarial=True,
+                                 temperature=1.0, uni_weight=False, uni_batch=Bg, g_out=g_g[:B], dq_out=dq_g[:B],
+                                 stats_out=st_g[:B])
+
+        def glob():
+            adam = opt.prepare_fused(m.entity_embedding, m.relation_embedding, None, write_grad=True)
+            ops.train_step_from_rows(desc, "tail-batch", pg, ng, wg, wsum, dev, uni_weight=False, uni_batch=Bg,
+                                     regularization=0.0, g_in=g_g, dq_in=dq_g, stats=st_g, grad_entity=ge,
+                                     grad_relation=gr, grad_modulus=gm, losses=losses, adam=adam)
+            opt.step()
+        if world == 1:
+            res["rows_slice_ms"] = timed(rows, a.reps)
+        for k in range(world):  # every row's factors filled once, as after the exchange
+            sl = slice(k * B, (k + 1) * B)
+            ops.train_rows_slice(desc, "tail-batch", pg[sl], ng[sl], wg[sl], wsum, dev, adversarial=True,
+                                 temperature=1.0, uni_weight=False, uni_batch=Bg, g_out=g_g[sl], dq_out=dq_g[sl],
+                                 stats_out=st_g[sl])
+        res[f"global_step_ms_N{world}"] = timed(glob, a.reps)
+        res[f"exchange_bytes_per_rank_N{world}"] = (B * Le + B * N + 4 * B) * 4 + B * (N + 3) * 8 + 4 * B
+    res["allreduce_bytes_per_rank_grads"] = {f"N{k}": 2 * (k - 1) / k * E * Le * 4 for k in (2, 4, 8)}
+    print(json.dumps(res), flush=True)
+
+
+if __name__ == "__main__":
+    main()
