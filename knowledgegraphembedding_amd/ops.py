@@ -220,6 +220,14 @@ def _train_ws(desc: _lib.ModelDesc, B: int, n: int, dev) -> torch.Tensor:
     return state(dev).workspace(need)
 
 
+def _check_row_buffers(dev, B: int, n: int, Le: int, g, dq, stats) -> None:
+    for t, shape in ((g, (B, n)), (dq, (B, Le)), (stats, (B, 4))):
+        if (tuple(t.shape) != shape or not t.is_contiguous() or t.dtype != torch.float32
+                or t.device != dev):
+            raise ValueError(f"row buffer {tuple(t.shape)} {t.dtype} on {t.device}: expected contiguous "
+                             f"float32 {shape} on {dev}")
+
+
 def train_rows_slice(desc: _lib.ModelDesc, mode: str, pos: torch.Tensor, neg: torch.Tensor, sub_w: torch.Tensor,
                      weight_sum_dev: Optional[torch.Tensor], dev, *, adversarial: bool, temperature: float,
                      uni_weight: bool, uni_batch: int, g_out: torch.Tensor, dq_out: torch.Tensor,
@@ -232,9 +240,7 @@ def train_rows_slice(desc: _lib.ModelDesc, mode: str, pos: torch.Tensor, neg: to
     pos, neg = _idx(pos, dev), _idx(neg, dev)
     w = sub_w.to(dev, dtype=torch.float32).contiguous().view(-1)
     B, n = neg.shape
-    for t, shape in ((g_out, (B, n)), (dq_out, (B, desc.entity_dim)), (stats_out, (B, 4))):
-        if tuple(t.shape) != shape or not t.is_contiguous() or t.dtype != torch.float32:
-            raise ValueError(f"row buffer of shape {tuple(t.shape)}, expected contiguous fp32 {shape}")
+    _check_row_buffers(dev, B, n, desc.entity_dim, g_out, dq_out, stats_out)
     ws = _train_ws(desc, B, n, dev)
     st = state(dev)
     _lib.check(_lib.load().kge_train_rows_slice(
@@ -252,9 +258,12 @@ def train_step_from_rows(desc: _lib.ModelDesc, mode: str, pos: torch.Tensor, neg
     """The rest of the step for the whole (gathered) batch from the exchanged
     row factors (kge_train_step_from_rows); bit-identical to one process
     running train_step_grads / the fused step on that batch."""
+    if mode not in ("head-batch", "tail-batch"):
+        raise ValueError("Training batch mode %s not supported" % mode)
     pos, neg = _idx(pos, dev), _idx(neg, dev)
     w = sub_w.to(dev, dtype=torch.float32).contiguous().view(-1)
     B, n = neg.shape
+    _check_row_buffers(dev, B, n, desc.entity_dim, g_in, dq_in, stats)
     ws = _train_ws(desc, B, n, dev)
     st = state(dev)
     _lib.check(_lib.load().kge_train_step_from_rows(
