@@ -55,10 +55,15 @@ TIMER_PERIOD = 8
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
 
 
-def algorithmic_row_bytes(b: int, n: int, le: int, lr: int) -> int:
-    """Bytes one fused row-pass launch must move: every negative
-    row once, the positive h/r/t rows, indices and weights."""
-    return b * n * le * 4 + b * (le + lr + le) * 4 + b * n * 8 + b * 3 * 8 + b * 4
+def algorithmic_row_bytes(b: int, n: int, le: int, lr: int, fused_tail: bool = True) -> int:
+    """Bytes one fused row-pass launch must move.  Reads: every
+    negative row once, the positive h/r/t rows, indices and weights.  Writes:
+    dL/ds [b, n], q [b, le] for the entity pass, the row statistics, and — with
+    the epilogue fused into the launch (the default) — the head/tail [2b, le]
+    and relation [b, lr] gradient contributions (else dL/dq [b, le])."""
+    reads = b * n * le * 4 + b * (le + lr + le) * 4 + b * n * 8 + b * 3 * 8 + b * 4
+    writes = b * n * 4 + b * le * 4 + b * 16 + ((2 * b * le + b * lr) * 4 if fused_tail else b * le * 4)
+    return reads + writes
 
 
 class DeviceBatches:
@@ -217,7 +222,7 @@ def main():
 
     calls = max(1.0, float(stage[6]))
     row_ms = float(stage[1]) / calls
-    row_bytes = algorithmic_row_bytes(B, NNEG, 2 * D, D)
+    row_bytes = algorithmic_row_bytes(B, NNEG, 2 * D, D, fused_tail=os.environ.get("KGE_FUSE_EPI", "1") != "0")
     achieved = row_bytes / (row_ms * 1e-3) / 1e9 if row_ms > 0 else None
     traffic = None
     tj = a.traffic_json or os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "pmc_traffic.json")
@@ -251,7 +256,7 @@ def main():
                      "csr_join": float(stage[3]) / calls, "entity_pass": float(stage[4]) / calls,
                      "relation_join_finalize": float(stage[5]) / calls,
                      "other_incl_adam_ms": dt / a.steps * 1e3 - float(stage[:6].sum()) / calls},
-        "roofline": {"bound": "hbm", "kernel": "k_row (fused negative scoring + self-adversarial loss)",
+        "roofline": {"bound": "hbm", "kernel": "k_row (q build + negative scoring + self-adversarial loss + q-side backward + positive epilogue)",
                      "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS if achieved else None,
                      "traffic": traffic, "algorithmic_bytes_per_launch": row_bytes,
                      "avg_launch_ms": row_ms},
