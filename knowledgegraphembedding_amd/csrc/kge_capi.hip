@@ -488,8 +488,8 @@ int kge_score(const kge_model_desc* m, int32_t mode, const int64_t* pos, const i
   int st = check_model(m, &geo);
   if (st) return st;
   if (mode != KGE_SINGLE && mode != KGE_HEAD_BATCH && mode != KGE_TAIL_BATCH) return KGE_ERR_MODE;
+  if (batch == 0 && nneg >= 1) return KGE_OK;  // empty batch: nothing to score (buffers may be empty/NULL)
   if (!pos || !out || !err_flag || batch < 0 || nneg < 1) return KGE_ERR_ARG;
-  if (batch == 0) return KGE_OK;
   ScoreArgs a;
   a.ent = m->entity_embedding; a.rel = m->relation_embedding; a.modulus = m->modulus;
   a.pos = pos;
