@@ -66,6 +66,27 @@ def algorithmic_row_bytes(b: int, n: int, le: int, lr: int, fused_tail: bool = T
     return reads + writes
 
 
+def step_roofline(step_s: float) -> dict:
+    """Whole-step HBM roofline: the bytes any fwd+bwd implementation must move
+    (read every negative/positive row, indices, weights; write each touched
+    gradient row once) and, separately, + a dense Adam over both tables
+    (param/grad/m/v read, param/m/v written = 28 B per element)."""
+    le, lr = 2 * D, D
+    fwd = B * NNEG * le * 4 + B * (le + lr + le) * 4 + B * NNEG * 8 + B * 3 * 8 + B * 4
+    fwd_bwd = fwd + B * (NNEG + 2) * le * 4 + B * lr * 4
+    adam = 28 * (E * le + R * lr)
+
+    def gbs(nbytes):
+        return nbytes / step_s / 1e9
+
+    return {"algorithmic_bytes_fwd_bwd": fwd_bwd, "achieved_fwd_bwd": gbs(fwd_bwd),
+            "frac_fwd_bwd": gbs(fwd_bwd) / HBM_PEAK_GBS,
+            "algorithmic_bytes_with_adam": fwd_bwd + adam, "achieved_with_adam": gbs(fwd_bwd + adam),
+            "frac_with_adam": gbs(fwd_bwd + adam) / HBM_PEAK_GBS, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "note": "algorithmic bytes / measured step time; the FB15k tables (120 MB) and part of the Adam "
+                    "state stay in the 256 MB Infinity Cache, so a fraction above 1 is fabric-side, not HBM"}
+
+
 class DeviceBatches:
     """Pre-staged device batches, tail-batch on odd steps and head-batch on even
     steps (dataloader.py:171-177)."""
@@ -260,6 +281,7 @@ def main():
                      "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS if achieved else None,
                      "traffic": traffic, "algorithmic_bytes_per_launch": row_bytes,
                      "avg_launch_ms": row_ms},
+        "step_roofline": step_roofline(dt / a.steps),
     }
     if a.workload != "fb15k":
         out["metric"] = f"scored (pos+neg) triples/sec, RotatE {a.workload} d={D} b={B} n={NNEG}"
