@@ -384,8 +384,7 @@ int run_grad(const kge_model_desc* m, const Geom& geo, int mode, const int64_t* 
   if (nsl > 0) {
     // 7: 4 rows in flight, Adam moments up front, packed RotatE math, non-temporal
     // row/Adam/gradient stream (measured best: entity pass 0.29 → 0.24 ms; 6 = same with plain loads/stores)
-    static const int pf = env_int("KGE_ENT_PF", 7);
-    ea.minw = pf;
+    ea.minw = env_int("KGE_ENT_PF", 7);  // read per call (tests switch it)
   }
   ea.slice_w = nsl > 0 ? (geo.eg.S + nsl - 1) / nsl : 0;
   ea.adam = adam_t(adam ? &adam->entity : nullptr);

@@ -440,7 +440,9 @@ def test_config2_full_size_properties():
                                       ("DistMult", 52, 700)])
 def test_entity_pass_column_slices_bitwise(name, d, B, monkeypatch):
     """The LDS-tiled entity pass (k_entity_tl, KGE_ENT_TILE=1), the column-sliced
-    pass (k_entity_sl, nsl = 1, 2, 4, 8 slices; the default) and the row-per-wave pass
+    pass (k_entity_sl, nsl = 1, 2, 4, 8 slices; the default), its software-pipelined form
+    (k_entity_pp, KGE_ENT_PF = 12..28: 1, 2, 4 or 8 entities per wave), its 30-32 register
+    budgets and the row-per-wave pass
     (KGE_ENT_TILE=0 KGE_ENT_SLICES=0) apply the same per-element arithmetic in
     the same occurrence order: identical gradients and fused Adam updates, bit
     for bit (the regulariser's partial sums only regroup).  d = 200 / 104 / 52
@@ -451,10 +453,14 @@ def test_entity_pass_column_slices_bitwise(name, d, B, monkeypatch):
     pos, neg, w = synth.kge_batch(88, B, n, E, R)
     P, N, W = torch.from_numpy(pos).to(DEV), torch.from_numpy(neg).to(DEV), torch.from_numpy(w).to(DEV)
     out = {}
-    variants = ("0", "1", "2", "4", "8", "tile") if d == 200 else ("0", "tile")
+    # "pf<k>": KGE_ENT_PF=k on 4 slices — k_entity_sl with other register budgets
+    # (30-32) and the software-pipelined k_entity_pp (12-28)
+    pipelined = ("pf12", "pf14", "pf21", "pf22", "pf24", "pf28", "pf30", "pf31", "pf32")
+    variants = (("0", "1", "2", "4", "8", "tile") if d == 200 else ("0", "tile")) + pipelined
     for nsl in variants:
         monkeypatch.setenv("KGE_ENT_TILE", "1" if nsl == "tile" else "0")
-        monkeypatch.setenv("KGE_ENT_SLICES", "0" if nsl == "tile" else nsl)
+        monkeypatch.setenv("KGE_ENT_SLICES", "0" if nsl == "tile" else ("4" if nsl.startswith("pf") else nsl))
+        monkeypatch.setenv("KGE_ENT_PF", nsl[2:] if nsl.startswith("pf") else "7")
         m, *_ = build_model(name, E, R, d, 12.0, 5)
         opt = KGEAdam([p for p in m.parameters() if p.requires_grad], lr=1e-3)
         res = []
