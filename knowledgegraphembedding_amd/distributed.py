@@ -17,7 +17,10 @@ normaliser is global: every rank
   4. steps the (replicated) optimizer identically.
 
 The regularisation term reads the full tables, so only rank 0 adds it before
-the sum (it would otherwise be counted world_size times).
+the sum (it would otherwise be counted world_size times).  Every rank must
+feed the same local batch size: the --uni_weight normaliser is taken as
+1 / (B_local * world) without a host round trip (the factor exchange's
+all-gathers require equal sizes anyway).
 
 Two exchanges implement step 3 (`dp_exchange_mode`):
 

@@ -95,10 +95,11 @@ def _worker(rank, world, port, name, adv, uni, reg, out):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("name,adv,uni,reg", [("RotatE", True, False, 0.0), ("ComplEx", False, True, 1e-3),
-                                              ("pRotatE", True, False, 0.0), ("DistMult", True, False, 1e-3)])
-def test_dp_two_ranks_match_global_batch(name, adv, uni, reg):
-    world = 2
+@pytest.mark.parametrize("name,adv,uni,reg,world", [("RotatE", True, False, 0.0, 2), ("ComplEx", False, True, 1e-3, 2),
+                                                    ("pRotatE", True, False, 0.0, 2), ("DistMult", True, False, 1e-3, 2),
+                                                    ("RotatE", True, False, 0.0, 4), ("TransE", False, True, 1e-3, 4)])
+def test_dp_ranks_match_global_batch(name, adv, uni, reg, world):
+    """world 2 and 4 (the driver's 4- and 8-GPU runs use this "grads" exchange)."""
     mgr = mp.Manager()
     out = mgr.dict()
     mp.spawn(_worker, args=(world, _free_port(), name, adv, uni, reg, out), nprocs=world, join=True)
@@ -168,9 +169,8 @@ def _fx_worker(rank, world, port, uni, out):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("uni", [False, True])
-def test_factor_exchange_gathers_global_batch(uni):
-    world = 2
+@pytest.mark.parametrize("uni,world", [(False, 2), (True, 2), (False, 4)])
+def test_factor_exchange_gathers_global_batch(uni, world):
     out = mp.Manager().dict()
     mp.spawn(_fx_worker, args=(world, _free_port(), uni, out), nprocs=world, join=True)
     pos, neg, w = (torch.from_numpy(x) for x in synth.kge_batch(5, B, N, E, R))
@@ -188,4 +188,5 @@ def test_factor_exchange_gathers_global_batch(uni):
             assert s["slice"][1] is None and s["global_scalars"][2] is None
         else:  # Σw of the GLOBAL weights, on both sides of the exchange
             assert s["slice"][1] == pytest.approx(float(w.sum())) and s["global_scalars"][2] == s["slice"][1]
-    assert torch.equal(out[0]["losses"], out[1]["losses"])
+    for rank in range(1, world):
+        assert torch.equal(out[0]["losses"], out[rank]["losses"])

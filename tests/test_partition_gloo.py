@@ -102,10 +102,11 @@ def _worker(rank, world, port, name, adv, uni, reg, out):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("name,adv,uni,reg", [("RotatE", True, False, 0.0), ("DistMult", False, True, 1e-3),
-                                              ("pRotatE", True, False, 0.0)])
-def test_row_partition_matches_single_process(name, adv, uni, reg):
-    world = 2
+@pytest.mark.parametrize("name,adv,uni,reg,world", [("RotatE", True, False, 0.0, 2), ("DistMult", False, True, 1e-3, 2),
+                                                    ("pRotatE", True, False, 0.0, 2), ("RotatE", True, False, 0.0, 3),
+                                                    ("ComplEx", False, False, 1e-3, 4)])
+def test_row_partition_matches_single_process(name, adv, uni, reg, world):
+    """world 2, 3 (E not a multiple of the world: a padded last shard) and 4."""
     mgr = mp.Manager()
     out = mgr.dict()
     mp.spawn(_worker, args=(world, _free_port(), name, adv, uni, reg, out), nprocs=world, join=True)
