@@ -381,11 +381,10 @@ int run_grad(const kge_model_desc* m, const Geom& geo, int mode, const int64_t* 
   }();
   ea.minw = ent_minw;
   ea.nsl = nsl;
-  if (nsl > 0) {
-    // 7: 4 rows in flight, Adam moments up front, packed RotatE math, non-temporal
-    // row/Adam/gradient stream (measured best: entity pass 0.29 → 0.24 ms; 6 = same with plain loads/stores)
-    ea.minw = env_int("KGE_ENT_PF", 7);  // read per call (tests switch it)
-  }
+  // SL_NT: 4 rows in flight, Adam moments up front, packed RotatE math, non-temporal
+  // row/Adam/gradient stream (measured best: entity pass 0.29 → 0.24 ms; SL_PACKED = same with
+  // plain loads/stores).  Read per call (tests switch it).
+  ea.slv = nsl > 0 ? env_int("KGE_ENT_PF", SL_NT) : SL_NT;
   ea.slice_w = nsl > 0 ? (geo.eg.S + nsl - 1) / nsl : 0;
   ea.adam = adam_t(adam ? &adam->entity : nullptr);
   ea.adamk = ak;
