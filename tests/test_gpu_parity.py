@@ -372,6 +372,33 @@ def test_ranks_vs_golden(g_ranks, golden_info, path, monkeypatch):
         print("  ", r)
 
 
+def test_protate_tile_ranks_vs_oracle_and_scan(monkeypatch):
+    """pRotatE's register tile scores sin(q − e) / sin(e + q) by the
+    angle-difference identity from staged (sin, cos) pairs.  Its ranks must
+    equal the oracle's strict-count rank on every query whose fp64 margin clears
+    the fp32 score tolerance, and the sinf-based wave scan (KGE_RANK_TILE=0) on
+    the same queries; E = 300 keeps most score gaps above that tolerance."""
+    E, R, d, gamma = 300, 7, 64, 12.0
+    m, ent, rel, mod, rng = build_model("pRotatE", E, R, d, gamma, 11)
+    rs = np.random.RandomState(5)
+    true = np.unique(np.stack([rs.randint(0, E, 900), rs.randint(0, R, 900), rs.randint(0, E, 900)], 1), axis=0)
+    test = true[rs.randint(0, len(true), 48)]
+    g = torch.Tensor([gamma]).item()
+    clear_total = 0
+    for mode in ("head-batch", "tail-batch"):
+        monkeypatch.setenv("KGE_RANK_TILE", "1")
+        tile, ties = m.rank_queries(test, true, mode)
+        monkeypatch.setenv("KGE_RANK_TILE", "0")
+        scan, _ = m.rank_queries(test, true, mode)
+        orc = O.filtered_ranks("pRotatE", torch.from_numpy(ent), torch.from_numpy(rel),
+                               None if mod is None else torch.from_numpy(mod), test, true, mode, g, rng)
+        clear = (orc["margin64"] > 1e-4 * np.maximum(1.0, np.abs(orc["score64"]))) & (ties == 0)
+        clear_total += int(clear.sum())
+        assert np.array_equal(tile[clear], orc["rank_count"][clear]), mode
+        assert np.array_equal(tile[clear], scan[clear]), mode
+    assert clear_total >= 30, clear_total
+
+
 def test_test_step_metrics_vs_golden(g_ranks, golden_info):
     kg = golden_info["ranks"][0]
     tag, E, R, d, seed = kg["tag"], kg["E"], kg["R"], kg["d"], kg["seed"]
