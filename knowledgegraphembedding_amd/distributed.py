@@ -43,6 +43,9 @@ import torch
 import torch.distributed as dist
 
 DP_CHUNKS = int(os.environ.get("KGE_DP_CHUNKS", "4"))
+# factor exchange: the rank's rows go through the row pass in this many pieces,
+# each piece's all-gather issued as soon as it is queued (overlaps the next piece)
+FX_CHUNKS = int(os.environ.get("KGE_FX_CHUNKS", "2"))
 
 
 def entity_chunks(nentity: int, chunks: int = DP_CHUNKS):
@@ -74,8 +77,8 @@ def dp_exchange_mode(world: int, override: str | None = None) -> str:
 _FX_BUFS: dict = {}
 
 
-def _fx_buffers(dev, Bg: int, n: int, Le: int):
-    key = (dev, Bg, n, Le)
+def _fx_buffers(dev, Bg: int, n: int, Le: int, tag: str = "global"):
+    key = (dev, Bg, n, Le, tag)
     b = _FX_BUFS.get(key)
     if b is None:
         b = _FX_BUFS[key] = (torch.empty(Bg, n, device=dev), torch.empty(Bg, Le, device=dev),
@@ -83,11 +86,20 @@ def _fx_buffers(dev, Bg: int, n: int, Le: int):
     return b
 
 
+def fx_pieces(B: int, chunks: int = FX_CHUNKS):
+    """Row ranges [r0, r1) of a rank's B rows for the overlapped factor gather
+    (equal pieces; one piece when B does not split evenly)."""
+    k = chunks if chunks > 1 and B % chunks == 0 else 1
+    step = B // k
+    return [(c * step, (c + 1) * step) for c in range(k)]
+
+
 def dp_train_step_factors(model, positive_sample, negative_sample, subsampling_weight, mode, args,
                           optimizer=None):
     """One data-parallel step by factor exchange (module docstring): Σw over the
     gathered weights, the row pass on this rank's rows into its place in the
-    gather buffers, an all-gather of those buffers, then the rest of the step
+    gather buffers (in FX_CHUNKS pieces, each piece's all-gather overlapping the
+    next piece's row pass), an all-gather of those buffers, then the rest of the step
     for the global batch on every rank (the fused Adam update included when the
     optimizer is a KGEAdam).  Returns the global [5] loss vector (the same on
     every rank, nothing left to reduce)."""
@@ -113,14 +125,39 @@ def dp_train_step_factors(model, positive_sample, negative_sample, subsampling_w
         wsum = torch.empty(1, device=dev)
         ops.weight_sum(w_g, wsum)  # the single-process Σw: same fixed order as the in-kernel sum
     desc = model.desc()
-    g_g, dq_g, st_g = _fx_buffers(dev, Bg, n, model.entity_dim)
-    sl = slice(r0, r0 + B)
-    ops.train_rows_slice(desc, mode, pos, neg, w_g[sl], wsum, dev,
-                         adversarial=bool(args.negative_adversarial_sampling),
-                         temperature=float(getattr(args, 'adversarial_temperature', 1.0)), uni_weight=uni,
-                         uni_batch=Bg, g_out=g_g[sl], dq_out=dq_g[sl], stats_out=st_g[sl])
-    for t in (g_g, dq_g, st_g):  # in place: this rank's rows are already at its slot
-        dist.all_gather_into_tensor(t, t[sl], group=group)
+    Le = model.entity_dim
+    g_g, dq_g, st_g = _fx_buffers(dev, Bg, n, Le)
+    pieces = fx_pieces(B)
+    if len(pieces) == 1:
+        sl = slice(r0, r0 + B)
+        ops.train_rows_slice(desc, mode, pos, neg, w_g[sl], wsum, dev,
+                             adversarial=bool(args.negative_adversarial_sampling),
+                             temperature=float(getattr(args, 'adversarial_temperature', 1.0)), uni_weight=uni,
+                             uni_batch=Bg, g_out=g_g[sl], dq_out=dq_g[sl], stats_out=st_g[sl])
+        for t in (g_g, dq_g, st_g):  # in place: this rank's rows are already at its slot
+            dist.all_gather_into_tensor(t, t[sl], group=group)
+    else:
+        # piece c of every rank is gathered into a [world, P, ...] staging slot
+        # while piece c+1 is computed, then scattered to rows r·B + c·P .. of
+        # the global buffers: same rows, same bits, the gather overlapped
+        P = pieces[0][1]
+        k = len(pieces)
+        stage = _fx_buffers(dev, Bg, n, Le, "stage")  # row c·world·P + r·P + j ↔ global row r·B + c·P + j
+        pending = []
+        for c, (a0, a1) in enumerate(pieces):
+            sg = slice(c * world * P, (c + 1) * world * P)
+            mine = slice(c * world * P + rank * P, c * world * P + (rank + 1) * P)
+            ops.train_rows_slice(desc, mode, pos[a0:a1], neg[a0:a1], w_g[r0 + a0:r0 + a1], wsum, dev,
+                                 adversarial=bool(args.negative_adversarial_sampling),
+                                 temperature=float(getattr(args, 'adversarial_temperature', 1.0)), uni_weight=uni,
+                                 uni_batch=Bg, g_out=stage[0][mine], dq_out=stage[1][mine], stats_out=stage[2][mine])
+            for t in stage:
+                pending.append(dist.all_gather_into_tensor(t[sg], t[mine], group=group, async_op=True))
+        for h in pending:
+            h.wait()
+        for t, dst in zip(stage, (g_g, dq_g, st_g)):
+            rest = t.shape[1:]
+            dst.view(world, k, P, *rest).copy_(t.view(k, world, P, *rest).transpose(0, 1))
     for h in ids:
         h.wait()
     adam = None
