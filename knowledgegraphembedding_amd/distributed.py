@@ -56,10 +56,32 @@ def entity_chunks(nentity: int, chunks: int = DP_CHUNKS):
 
 
 def dp_allreduce_(tensors, group=None) -> None:
-    """In-place SUM all-reduce of a list of tensors (one collective per tensor;
-    RCCL runs them on its own stream in issue order)."""
-    for t in tensors:
-        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+    """In-place SUM all-reduce of a list of tensors as ONE collective over
+    their concatenation (the small relation/modulus gradients and the loss
+    partials would otherwise each pay a collective's fixed latency)."""
+    finish = dp_allreduce_packed_async(tensors, group)
+    finish()
+
+
+def dp_allreduce_packed_async(tensors, group=None):
+    """Issue one async SUM all-reduce over the concatenation of `tensors`;
+    returns a callable that waits for it and copies the sums back in place.
+    The copy-back is elementwise, so the sums are those of separate
+    all-reduces."""
+    tensors = [t for t in tensors if t is not None]
+    if not tensors:
+        return lambda: None
+    flat = torch.cat([t.reshape(-1).float() for t in tensors])
+    work = dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=group, async_op=True)
+
+    def finish():
+        work.wait()
+        off = 0
+        for t in tensors:
+            n = t.numel()
+            t.copy_(flat[off:off + n].view_as(t))
+            off += n
+    return finish
 
 
 def dp_exchange_mode(world: int, override: str | None = None) -> str:
@@ -208,14 +230,15 @@ def dp_train_grads(model, positive_sample, negative_sample, subsampling_weight, 
     rest = [model.relation_embedding.grad]
     if model.model_name == 'pRotatE' and model.modulus.grad is not None:
         rest.append(model.modulus.grad)
-    for t in rest + [losses]:
-        pending.append(dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group, async_op=True))
+    # relation (+ modulus) gradient and the loss partials: one packed collective
+    finish_rest = dp_allreduce_packed_async(rest + [losses], group)
     if optimizer is not None and hasattr(optimizer, 'step_param') and model.entity_embedding.requires_grad:
         # Adam on each entity-row chunk as soon as its reduction lands, while
         # the later chunks are still on the wire
         optimizer.step_param(model.entity_embedding, chunks, before_chunk=lambda k: pending[k].wait())
     for work in pending:  # (waiting twice on a chunk is a no-op)
         work.wait()
+    finish_rest()
     # loss = (pos + neg) / 2 + reg must be recomputed from the summed parts
     losses[2] = (losses[0] + losses[1]) / 2 + losses[3]
     return losses
