@@ -2,6 +2,8 @@
 // counting sort), relation-gradient row sums, loss finalisation, Σw and Adam.
 #include <rocprim/device/device_scan.hpp>
 
+#include <cstdlib>
+
 #include "kge_common.h"
 #include "kge_rel.h"
 
@@ -156,22 +158,49 @@ __global__ __launch_bounds__(256) void k_weight_sum(const float* __restrict__ w,
 
 // ------------------------------------------------------------------ Adam
 // Standalone dense Adam over one tensor (KGEAdam.step / kge_adam_step).
+// NT: non-temporal (streaming) loads/stores — every byte is touched once.
+// U: float4 groups per thread and iteration (loads of all U issued first).
+template <bool NT>
+__device__ __forceinline__ float4 ld4(const float* base, int64_t i) {
+  if constexpr (NT) {
+    const tf4 v = __builtin_nontemporal_load(reinterpret_cast<const tf4*>(base) + i);
+    return make_float4(v.x, v.y, v.z, v.w);
+  } else {
+    return reinterpret_cast<const float4*>(base)[i];
+  }
+}
+template <bool NT>
+__device__ __forceinline__ void st4(float* base, int64_t i, const float4& x) {
+  if constexpr (NT) __builtin_nontemporal_store(tf4{x.x, x.y, x.z, x.w}, reinterpret_cast<tf4*>(base) + i);
+  else reinterpret_cast<float4*>(base)[i] = x;
+}
+template <bool NT, int U>
 __global__ __launch_bounds__(256) void k_adam(float* __restrict__ p, const float* __restrict__ g,
                                               float* __restrict__ m, float* __restrict__ v, int64_t n, AdamK k,
                                               float step_size, float bc2s) {
   const int64_t n4 = n / 4;
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
-    float4 P = reinterpret_cast<float4*>(p)[i];
-    const float4 G = reinterpret_cast<const float4*>(g)[i];
-    float4 Mv = reinterpret_cast<float4*>(m)[i];
-    float4 Vv = reinterpret_cast<float4*>(v)[i];
-    adam_elem(P.x, G.x, Mv.x, Vv.x, k, step_size, bc2s);
-    adam_elem(P.y, G.y, Mv.y, Vv.y, k, step_size, bc2s);
-    adam_elem(P.z, G.z, Mv.z, Vv.z, k, step_size, bc2s);
-    adam_elem(P.w, G.w, Mv.w, Vv.w, k, step_size, bc2s);
-    reinterpret_cast<float4*>(p)[i] = P;
-    reinterpret_cast<float4*>(m)[i] = Mv;
-    reinterpret_cast<float4*>(v)[i] = Vv;
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  for (int64_t i0 = (int64_t)blockIdx.x * 256 + threadIdx.x; i0 < n4; i0 += stride * U) {
+    float4 P[U], G[U], Mv[U], Vv[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t i = i0 + u * stride;
+      if (i < n4) {
+        P[u] = ld4<NT>(p, i); G[u] = ld4<NT>(g, i); Mv[u] = ld4<NT>(m, i); Vv[u] = ld4<NT>(v, i);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t i = i0 + u * stride;
+      if (i >= n4) continue;
+      adam_elem(P[u].x, G[u].x, Mv[u].x, Vv[u].x, k, step_size, bc2s);
+      adam_elem(P[u].y, G[u].y, Mv[u].y, Vv[u].y, k, step_size, bc2s);
+      adam_elem(P[u].z, G[u].z, Mv[u].z, Vv[u].z, k, step_size, bc2s);
+      adam_elem(P[u].w, G[u].w, Mv[u].w, Vv[u].w, k, step_size, bc2s);
+      st4<NT>(p, i, P[u]);
+      st4<NT>(m, i, Mv[u]);
+      st4<NT>(v, i, Vv[u]);
+    }
   }
   for (int64_t i = n4 * 4 + (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
     float P = p[i], Mv = m[i], Vv = v[i];
@@ -181,6 +210,11 @@ __global__ __launch_bounds__(256) void k_adam(float* __restrict__ p, const float
 }
 
 // ------------------------------------------------------------ launchers
+static int env_int_c(const char* name, int dflt) {  // read per call (A/B knobs)
+  const char* e = getenv(name);
+  return e ? atoi(e) : dflt;
+}
+
 static inline unsigned grid_for(int64_t n, unsigned cap = 4096) {
   int64_t g = (n + 255) / 256;
   if (g < 1) g = 1;
@@ -256,7 +290,20 @@ int launch_adam(float* p, const float* g, float* m, float* v, int64_t n, float b
                 float step_size, float bc2s, hipStream_t s) {
   AdamK k;
   k.b1 = b1; k.b2 = b2; k.eps = eps;
-  hipLaunchKernelGGL(k_adam, dim3(grid_for((n + 3) / 4, 8192)), dim3(256), 0, s, p, g, m, v, n, k, step_size, bc2s);
+  // KGE_ADAM_VARIANT: 2 (default) non-temporal + 2 float4 groups per thread and
+  // iteration: 5.6 TB/s on the FB15k table against 5.0-5.2 for plain float4 (0);
+  // 1 non-temporal only, 3 two groups only (tools/dbg/adam_rate.py,
+  // profiles/r01/adam_rate_variants.jsonl).  Same per-element math in all.
+  const int var = env_int_c("KGE_ADAM_VARIANT", 2);
+  const dim3 grid(grid_for((n + 3) / 4, 8192));
+  if (var == 1)
+    hipLaunchKernelGGL((k_adam<true, 1>), grid, dim3(256), 0, s, p, g, m, v, n, k, step_size, bc2s);
+  else if (var == 2)
+    hipLaunchKernelGGL((k_adam<true, 2>), grid, dim3(256), 0, s, p, g, m, v, n, k, step_size, bc2s);
+  else if (var == 3)
+    hipLaunchKernelGGL((k_adam<false, 2>), grid, dim3(256), 0, s, p, g, m, v, n, k, step_size, bc2s);
+  else
+    hipLaunchKernelGGL((k_adam<false, 1>), grid, dim3(256), 0, s, p, g, m, v, n, k, step_size, bc2s);
   return (int)hipGetLastError();
 }
 

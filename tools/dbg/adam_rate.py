@@ -28,9 +28,11 @@ def timed(fn, reps=20):
 for name, rows in (("fb15k", 14951), ("yago3-10", 123182)):
     n = rows * 2000
     p, g, m, v = (torch.rand(n, device=dev) for _ in range(4))
-    t = timed(lambda: ops.adam_step(p, g, m, v, step=3, lr=1e-4, beta1=0.9, beta2=0.999, eps=1e-8))
-    print(json.dumps({"case": name, "kernel": "kge_adam_step", "elems": n, "bytes": 28 * n, "ms": t * 1e3,
-                      "GBps": 28 * n / t / 1e9}), flush=True)
+    for var in ("0", "1", "2", "3", "0"):  # KGE_ADAM_VARIANT (kge_common.hip k_adam)
+        os.environ["KGE_ADAM_VARIANT"] = var
+        t = timed(lambda: ops.adam_step(p, g, m, v, step=3, lr=1e-4, beta1=0.9, beta2=0.999, eps=1e-8))
+        print(json.dumps({"case": name, "kernel": "kge_adam_step", "variant": var, "elems": n, "bytes": 28 * n,
+                          "ms": t * 1e3, "GBps": 28 * n / t / 1e9}), flush=True)
     dst = torch.empty_like(p)
     t = timed(lambda: dst.copy_(p))
     print(json.dumps({"case": name, "kernel": "torch copy_", "bytes": 8 * n, "ms": t * 1e3,
