@@ -247,7 +247,7 @@ int run_grad(const kge_model_desc* m, const Geom& geo, int mode, const int64_t* 
   const int write_grad = (!adam || adam->write_grad) ? 1 : 0;
   const Consts c = consts_of(m);
   const int Le = m->entity_dim, Lr = m->relation_dim;
-  const size_t lds = sizeof(float) * (2 * 64 * (size_t)geo.ns * geo.vec + (size_t)vb_floats(Le) + (size_t)ra.n_lds + 32);
+  const size_t lds = sizeof(float) * (2 * 64 * (size_t)geo.ns * geo.vec + (size_t)vb_floats(Le, 64 * geo.ns * geo.vec) + (size_t)ra.n_lds + 32);
   if (lds > 64 * 1024) return KGE_ERR_DIM;
   const bool all = (phases == KGE_PHASE_ALL);
   if (e_end < 0) e_end = m->nentity;
@@ -446,11 +446,7 @@ RowArgs row_args(const kge_model_desc* m, const Geom& geo, const int64_t* pos, c
   ra.Le = m->entity_dim; ra.Lr = m->relation_dim; ra.eg = geo.eg; ra.c = consts_of(m);
   ra.g_out = w.g; ra.q_out = w.q; ra.dq_out = w.dq; ra.ent_contrib = w.ent_contrib; ra.rel_contrib = w.rel_contrib;
   ra.row_stats = w.row_stats; ra.err = err;
-  static const int pipe = [] {
-    const char* e = getenv("KGE_ROW_PIPE");
-    return e ? atoi(e) : 0;
-  }();
-  ra.pipe = pipe;
+  ra.pipe = env_int("KGE_ROW_PIPE", 0);  // read per call (tests switch it)
   ra.fuse_q = env_int("KGE_FUSE_Q", 1);  // measured +1.8 %; bit-identical to the separate k_build_q
   ra.fuse_epi = env_int("KGE_FUSE_EPI", 1);  // measured +1 % once k_row's RotatE math went to register pairs (no spills)
   return ra;

@@ -64,7 +64,12 @@ struct RowArgs {
 
 // k_row's LDS merge buffer: [2][Le] floats, and at least the 256 floats the
 // fused Σw reduction (block_weight_sum) uses as its tree
-__host__ __device__ inline int vb_floats(int Le) { return 2 * Le > 256 ? 2 * Le : 256; }
+// k_row's merge buffer: 2 rows of Le (merge), >= 256 (Σw tree), >= 4 padded
+// half-rows of qp floats (the HP variant's per-wave V im halves)
+__host__ __device__ inline int vb_floats(int Le, int qp) {
+  int v = 2 * Le > 256 ? 2 * Le : 256;
+  return v > 4 * qp ? v : 4 * qp;
+}
 
 struct RelArgs {
   const float* rel;

@@ -512,14 +512,21 @@ def test_fused_q_build_bitwise(name, E, d, B, n, monkeypatch):
     same fixed-order Σw reduction, same epilogue function).  Many blocks per
     launch (B = 64, 300) exercise the fused tail's c_i, which must not read the
     Σw that block 0 publishes in the same launch; d = 16 with B = 300 needs the
-    Σw tree's 256 floats of LDS beyond the 2·Le merge buffer."""
+    Σw tree's 256 floats of LDS beyond the 2·Le merge buffer.  The row-pass
+    pipelines (KGE_ROW_PIPE = 1, 2) must give the same bits as well."""
     R = 9
     pos, neg, w = synth.kge_batch(91, B, n, E, R)
     P, N, W = torch.from_numpy(pos).to(DEV), torch.from_numpy(neg).to(DEV), torch.from_numpy(w).to(DEV)
     res = {}
-    for fq in ("0", "1", "epi"):
-        monkeypatch.setenv("KGE_FUSE_Q", "0" if fq == "0" else "1")
-        monkeypatch.setenv("KGE_FUSE_EPI", "1" if fq == "epi" else "0")
+    # + the row-pass pipelines: "hp" = KGE_ROW_PIPE=2 (RotatE: V's im half in
+    # LDS, next row's re half in flight; fused), "hp0" the same unfused, "pipe"
+    # = KGE_ROW_PIPE=1 (whole next row in registers)
+    variants = {"0": ("0", "0", "0"), "1": ("1", "0", "0"), "epi": ("1", "1", "0"), "hp": ("1", "1", "2"),
+                "hp0": ("0", "0", "2"), "pipe": ("0", "0", "1")}
+    for fq, (fuse_q, fuse_epi, pipe) in variants.items():
+        monkeypatch.setenv("KGE_FUSE_Q", fuse_q)
+        monkeypatch.setenv("KGE_FUSE_EPI", fuse_epi)
+        monkeypatch.setenv("KGE_ROW_PIPE", pipe)
         out = []
         for adv, uni in ((True, False), (False, True)):
             m, *_ = build_model(name, E, R, d, 12.0, 7)
@@ -533,7 +540,7 @@ def test_fused_q_build_bitwise(name, E, d, B, n, monkeypatch):
             losses = m.compute_train_grads(P, N, W, "tail-batch", args, weight_sum=W.sum().reshape(1))
             out.append([losses.detach().cpu().clone(), m.entity_embedding.grad.cpu().clone()])
         res[fq] = out
-    for variant in ("1", "epi"):
+    for variant in list(variants)[1:]:
         for a, b in zip(res["0"], res[variant]):
             for x, y in zip(a, b):
                 assert torch.equal(x, y), variant
