@@ -97,9 +97,11 @@ def _worker(rank, world, port, name, adv, uni, reg, out):
 
 @pytest.mark.parametrize("name,adv,uni,reg,world", [("RotatE", True, False, 0.0, 2), ("ComplEx", False, True, 1e-3, 2),
                                                     ("pRotatE", True, False, 0.0, 2), ("DistMult", True, False, 1e-3, 2),
-                                                    ("RotatE", True, False, 0.0, 4), ("TransE", False, True, 1e-3, 4)])
+                                                    ("RotatE", True, False, 0.0, 4), ("TransE", False, True, 1e-3, 4),
+                                                    ("DistMult", True, False, 1e-3, 8)])
 def test_dp_ranks_match_global_batch(name, adv, uni, reg, world):
-    """world 2 and 4 (the driver's 4- and 8-GPU runs use this "grads" exchange)."""
+    """world 2, 4 and 8 (the driver's 4- and 8-GPU runs use this "grads" exchange;
+    at 8 ranks each holds one positive of the global batch)."""
     mgr = mp.Manager()
     out = mgr.dict()
     mp.spawn(_worker, args=(world, _free_port(), name, adv, uni, reg, out), nprocs=world, join=True)
