@@ -251,6 +251,14 @@ def main():
         with open(tj) as f:
             traffic = json.load(f).get("hbm_bytes_per_launch")
 
+    ceiling = None  # k_row's access pattern alone (tools/dbg/gather_ceiling.hip), measured on MI355X
+    cj = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r01", "gather_ceiling.jsonl")
+    if a.workload == "fb15k" and os.path.exists(cj) and achieved:
+        with open(cj) as f:
+            c0 = json.loads(f.readline())
+        ceiling = {"GBps": c0["GBps"], "frac": achieved / c0["GBps"], "source": "profiles/r01/gather_ceiling.jsonl",
+                   "what": "same grid and buffer loads over the same table, no arithmetic"}
+
     value = a.steps * B * (NNEG + 1) * world / dt
     out = {
         "metric": METRIC,
@@ -280,7 +288,7 @@ def main():
         "roofline": {"bound": "hbm", "kernel": "k_row (q build + negative scoring + self-adversarial loss + q-side backward + positive epilogue)",
                      "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS if achieved else None,
                      "traffic": traffic, "algorithmic_bytes_per_launch": row_bytes,
-                     "avg_launch_ms": row_ms},
+                     "avg_launch_ms": row_ms, "pattern_ceiling": ceiling},
         "step_roofline": step_roofline(dt / a.steps),
     }
     if a.workload != "fb15k":
