@@ -230,6 +230,23 @@ int kge_train_step_from_rows(const kge_model_desc *m, int32_t mode, const int64_
                              float *grad_entity, float *grad_relation, float *grad_modulus, float *losses_out,
                              void *workspace, size_t workspace_bytes, int32_t *err_flag, void *stream);
 
+/*
+ * The same split with the occurrence CSR built ahead: kge_train_csr builds
+ * the CSR of the (gathered) batch into the workspace on `stream` — it needs
+ * only the ids, so a rank runs it while the factors are still on the wire —
+ * and kge_train_step_from_rows_csr is kge_train_step_from_rows reading that
+ * CSR instead of building it (same workspace, same batch).  Bit-identical.
+ */
+int kge_train_csr(const kge_model_desc *m, int32_t mode, const int64_t *pos, const int64_t *neg, int64_t batch,
+                  int64_t nneg, void *workspace, size_t workspace_bytes, int32_t *err_flag, void *stream);
+int kge_train_step_from_rows_csr(const kge_model_desc *m, int32_t mode, const int64_t *pos, const int64_t *neg,
+                                 int64_t batch, int64_t nneg, const float *subsampling_weight,
+                                 const float *weight_sum, int32_t uni_weight, int64_t uni_batch,
+                                 float regularization, const float *g_in, const float *dq_in, float *stats_inout,
+                                 const kge_adam_desc *adam, float *grad_entity, float *grad_relation,
+                                 float *grad_modulus, float *losses_out, void *workspace, size_t workspace_bytes,
+                                 int32_t *err_flag, void *stream);
+
 
 /*
  * Σ subsampling_weight into *out (device scalar) — the denominator of

@@ -94,6 +94,12 @@ SIGNATURES = {
         [_DESC, _I32, _P, _P, _I64, _I64, _P, _P, _I32, _I64, _F, _P, _P, _P, C.POINTER(AdamDesc), _P, _P, _P, _P,
          _P, _SZ, _P, _P],
     ),
+    "kge_train_csr": (C.c_int, [_DESC, _I32, _P, _P, _I64, _I64, _P, _SZ, _P, _P]),
+    "kge_train_step_from_rows_csr": (
+        C.c_int,
+        [_DESC, _I32, _P, _P, _I64, _I64, _P, _P, _I32, _I64, _F, _P, _P, _P, C.POINTER(AdamDesc), _P, _P, _P, _P,
+         _P, _SZ, _P, _P],
+    ),
     "kge_weight_sum": (C.c_int, [_P, _I64, _P, _P]),
     "kge_adam_step": (C.c_int, [_P, _P, _P, _P, _I64, _F, _F, _F, _F, _F, _P]),
     "kge_rank_workspace_bytes": (_SZ, [_DESC, _I64]),

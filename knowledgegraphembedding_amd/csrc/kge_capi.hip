@@ -221,7 +221,9 @@ Side* side_for_device() {
 }
 
 // Data-parallel factor exchange (kge_train_rows_slice / kge_train_step_from_rows)
-enum XStage : int { XS_NONE = 0, XS_ROWS_ONLY = 1, XS_FROM_ROWS = 2 };
+// XS_CSR_ONLY: the occurrence CSR of a batch alone, on the caller's stream;
+// XS_FROM_ROWS_CSR: XS_FROM_ROWS with that CSR already in the workspace
+enum XStage : int { XS_NONE = 0, XS_ROWS_ONLY = 1, XS_FROM_ROWS = 2, XS_CSR_ONLY = 3, XS_FROM_ROWS_CSR = 4 };
 
 // Shared body of backward and train.  Caller's stream: q build → gather loop →
 // epilogue → entity pass → finalise; side stream: CSR ∥ row pass, relation pass ∥ entity pass.
@@ -254,7 +256,9 @@ int run_grad(const kge_model_desc* m, const Geom& geo, int mode, const int64_t* 
   // stage timing: a full call records all 7 marks; a phased ROWS call (the
   // data-parallel path) records the row-pass marks and pads the rest, so the
   // row pass is timed live on every rank either way
-  const bool timed = (phases & KGE_PHASE_ROWS) && xstage != XS_FROM_ROWS && g_timer.on && ra.op == ROW_TRAIN &&
+  const bool from_rows = (xstage == XS_FROM_ROWS || xstage == XS_FROM_ROWS_CSR);
+  const bool csr_ready = (xstage == XS_FROM_ROWS_CSR);
+  const bool timed = (phases & KGE_PHASE_ROWS) && !from_rows && xstage != XS_CSR_ONLY && g_timer.on && ra.op == ROW_TRAIN &&
                      (g_timer.seen++ % (size_t)g_timer.period) == 0;
   ra.timer_mid = timed ? &timer_mark : nullptr;
   Side* sd = side_for_device();
@@ -316,33 +320,36 @@ int run_grad(const kge_model_desc* m, const Geom& geo, int mode, const int64_t* 
       for (int k = 0; k < 5; ++k) g_timer.mark(s);  // row-pass end + the stages not in this call
     return KGE_OK;
   }
-  if (xstage == XS_FROM_ROWS) ra.fuse_epi = 0;  // the epilogue reads the gathered dL/dq (k_row_epi)
-
-  if (phases & KGE_PHASE_ROWS) {
-  // fork point: the occurrence CSR needs only the batch indices (recorded
-  // before anything else is queued, so the side stream never waits for the
-  // row pass)
-  if (sd) hipEventRecord(sd->fork, s);
-
-  // q build + gather loop on the caller's stream, launched first so the GPU
-  // is on the long kernel while the host queues everything else
-  if (timed) g_timer.mark(s);
-  // (XS_FROM_ROWS: the row pass ran on the ranks; only q is rebuilt here)
-  st = launch_status(op.row(mode, geo.vec, geo.ns, xstage == XS_FROM_ROWS ? 2 : 0, ra, lds, s));
-  if (st) return st;
-  if (timed) g_timer.mark(s);
-
   CsrArgs ca;
   ca.pos = pos; ca.neg = neg; ca.neg_stride = neg_stride;
   ca.B = B; ca.n = n; ca.Bn = B * n; ca.E = m->nentity; ca.R = m->nrelation;
   ca.keys = w.keys; ca.cnt = w.cnt; ca.off = w.off; ca.tmp = w.tmp; ca.occ = w.occ; ca.err = err;
   ca.scan_tmp = w.scan_tmp; ca.scan_tmp_bytes = w.scan_tmp_bytes;
-  if (sd) hipStreamWaitEvent(ss, sd->fork, 0);
-  st = launch_status(launch_csr(ca, ss));
-  if (st) return st;
-  if (sd) hipEventRecord(sd->csr_done, ss);
+  if (xstage == XS_CSR_ONLY) return launch_status(launch_csr(ca, s));  // kge_train_csr
+  if (from_rows) ra.fuse_epi = 0;  // the epilogue reads the gathered dL/dq (k_row_epi)
 
-  if (sd && sch.csr_join_early && all) hipStreamWaitEvent(s, sd->csr_done, 0);
+  if (phases & KGE_PHASE_ROWS) {
+  // fork point: the occurrence CSR needs only the batch indices (recorded
+  // before anything else is queued, so the side stream never waits for the
+  // row pass)
+  if (sd && !csr_ready) hipEventRecord(sd->fork, s);
+
+  // q build + gather loop on the caller's stream, launched first so the GPU
+  // is on the long kernel while the host queues everything else
+  if (timed) g_timer.mark(s);
+  // (XS_FROM_ROWS: the row pass ran on the ranks; only q is rebuilt here)
+  st = launch_status(op.row(mode, geo.vec, geo.ns, from_rows ? 2 : 0, ra, lds, s));
+  if (st) return st;
+  if (timed) g_timer.mark(s);
+
+  if (!csr_ready) {
+    if (sd) hipStreamWaitEvent(ss, sd->fork, 0);
+    st = launch_status(launch_csr(ca, ss));
+    if (st) return st;
+    if (sd) hipEventRecord(sd->csr_done, ss);
+  }
+
+  if (sd && sch.csr_join_early && all && !csr_ready) hipStreamWaitEvent(s, sd->csr_done, 0);
   // epilogue (positive score, chain rule)
   st = launch_status(op.row(mode, geo.vec, geo.ns, 1, ra, lds, s));
   if (st) return st;
@@ -364,7 +371,8 @@ int run_grad(const kge_model_desc* m, const Geom& geo, int mode, const int64_t* 
   }  // KGE_PHASE_ROWS
 
   if (phases & KGE_PHASE_ENTITY) {
-  if (sd && !(all && sch.csr_join_early)) hipStreamWaitEvent(s, sd->csr_done, 0);  // join 1: the entity pass reads the CSR
+  if (sd && !(all && sch.csr_join_early) && !csr_ready)
+    hipStreamWaitEvent(s, sd->csr_done, 0);  // join 1: the entity pass reads the CSR
   if (timed) g_timer.mark(s);
 
   EntArgs ea;
@@ -567,8 +575,10 @@ static int train_impl(const kge_model_desc* m, int32_t mode, const int64_t* pos,
   if (st) return st;
   if (mode != KGE_HEAD_BATCH && mode != KGE_TAIL_BATCH) return KGE_ERR_MODE;
   if (xstage == XS_NONE && (!grad_entity || !grad_relation || !losses_out)) return KGE_ERR_ARG;
-  if (xstage != XS_NONE && (!rows_g || !rows_dq || !rows_stats)) return KGE_ERR_ARG;
-  if (xstage == XS_FROM_ROWS && (!grad_entity || !grad_relation || !losses_out)) return KGE_ERR_ARG;
+  const bool csr_only = (xstage == XS_CSR_ONLY);
+  const bool from_rows = (xstage == XS_FROM_ROWS || xstage == XS_FROM_ROWS_CSR);
+  if (xstage != XS_NONE && !csr_only && (!rows_g || !rows_dq || !rows_stats)) return KGE_ERR_ARG;
+  if (from_rows && (!grad_entity || !grad_relation || !losses_out)) return KGE_ERR_ARG;
   if (!pos || !neg || !err_flag || batch < 1 || nneg < 1) return KGE_ERR_ARG;
   if (adam) {
     if (!adam->entity.param || !adam->entity.exp_avg || !adam->entity.exp_avg_sq || !adam->relation.param ||
@@ -579,12 +589,12 @@ static int train_impl(const kge_model_desc* m, int32_t mode, const int64_t* pos,
     if (m->model == KGE_PROTATE && adam->modulus.param && adam->modulus.param != m->modulus) return KGE_ERR_ARG;
   }
   if (!uni_weight && !subsampling_weight) return KGE_ERR_ARG;
-  if (m->model == KGE_PROTATE && !grad_modulus && xstage != XS_ROWS_ONLY) return KGE_ERR_ARG;
-  if (xstage != XS_NONE && !uni_weight && !weight_sum) return KGE_ERR_ARG;  // the global Σw comes from the caller
+  if (m->model == KGE_PROTATE && !grad_modulus && xstage != XS_ROWS_ONLY && !csr_only) return KGE_ERR_ARG;
+  if (xstage != XS_NONE && !csr_only && !uni_weight && !weight_sum) return KGE_ERR_ARG;  // the global Σw comes from the caller
   size_t need = 0;
   GradWs w = carve_grad(workspace, m, batch, nneg, &need);
   if (!workspace || workspace_bytes < need) return KGE_ERR_WORKSPACE;
-  if (xstage != XS_NONE) {  // the exchanged per-row factors live in the caller's (gathered) buffers
+  if (xstage != XS_NONE && !csr_only) {  // the exchanged per-row factors live in the caller's (gathered) buffers
     w.g = rows_g;
     w.dq = rows_dq;
     w.row_stats = rows_stats;
@@ -644,6 +654,24 @@ int kge_train_step_from_rows(const kge_model_desc* m, int32_t mode, const int64_
   return train_impl(m, mode, pos, neg, batch, nneg, subsampling_weight, weight_sum, uni_weight, uni_batch, 1, 1.f,
                     regularization, adam, grad_entity, grad_relation, grad_modulus, losses_out, workspace,
                     workspace_bytes, err_flag, stream, KGE_PHASE_ALL, 0, -1, XS_FROM_ROWS, const_cast<float*>(g_in),
+                    const_cast<float*>(dq_in), stats_inout);
+}
+
+int kge_train_csr(const kge_model_desc* m, int32_t mode, const int64_t* pos, const int64_t* neg, int64_t batch,
+                  int64_t nneg, void* workspace, size_t workspace_bytes, int32_t* err_flag, void* stream) {
+  return train_impl(m, mode, pos, neg, batch, nneg, nullptr, nullptr, 1, 0, 1, 1.f, 0.f, nullptr, nullptr, nullptr,
+                    nullptr, nullptr, workspace, workspace_bytes, err_flag, stream, KGE_PHASE_ALL, 0, -1, XS_CSR_ONLY);
+}
+
+int kge_train_step_from_rows_csr(const kge_model_desc* m, int32_t mode, const int64_t* pos, const int64_t* neg,
+                                 int64_t batch, int64_t nneg, const float* subsampling_weight, const float* weight_sum,
+                                 int32_t uni_weight, int64_t uni_batch, float regularization, const float* g_in,
+                                 const float* dq_in, float* stats_inout, const kge_adam_desc* adam, float* grad_entity,
+                                 float* grad_relation, float* grad_modulus, float* losses_out, void* workspace,
+                                 size_t workspace_bytes, int32_t* err_flag, void* stream) {
+  return train_impl(m, mode, pos, neg, batch, nneg, subsampling_weight, weight_sum, uni_weight, uni_batch, 1, 1.f,
+                    regularization, adam, grad_entity, grad_relation, grad_modulus, losses_out, workspace,
+                    workspace_bytes, err_flag, stream, KGE_PHASE_ALL, 0, -1, XS_FROM_ROWS_CSR, const_cast<float*>(g_in),
                     const_cast<float*>(dq_in), stats_inout);
 }
 

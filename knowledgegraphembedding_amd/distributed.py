@@ -46,6 +46,8 @@ DP_CHUNKS = int(os.environ.get("KGE_DP_CHUNKS", "4"))
 # factor exchange: the rank's rows go through the row pass in this many pieces,
 # each piece's all-gather issued as soon as it is queued (overlaps the next piece)
 FX_CHUNKS = int(os.environ.get("KGE_FX_CHUNKS", "2"))
+# ... and the global batch's occurrence CSR is built on a side stream as soon as its ids arrive
+FX_CSR_AHEAD = os.environ.get("KGE_FX_CSR_AHEAD", "1") == "1"
 
 
 def entity_chunks(nentity: int, chunks: int = DP_CHUNKS):
@@ -108,6 +110,19 @@ def _fx_buffers(dev, Bg: int, n: int, Le: int, tag: str = "global"):
     return b
 
 
+_CSR_STREAMS: dict = {}
+
+
+def _csr_stream(dev):
+    """A side stream per device for the factor exchange's CSR (None on CPU)."""
+    if dev.type != "cuda":
+        return None
+    st = _CSR_STREAMS.get(dev)
+    if st is None:
+        st = _CSR_STREAMS[dev] = torch.cuda.Stream(dev)
+    return st
+
+
 def fx_pieces(B: int, chunks: int = FX_CHUNKS):
     """Row ranges [r0, r1) of a rank's B rows for the overlapped factor gather
     (equal pieces; one piece when B does not split evenly)."""
@@ -147,6 +162,21 @@ def dp_train_step_factors(model, positive_sample, negative_sample, subsampling_w
         wsum = torch.empty(1, device=dev)
         ops.weight_sum(w_g, wsum)  # the single-process Σw: same fixed order as the in-kernel sum
     desc = model.desc()
+    # the global batch's occurrence CSR needs only the ids: built on a side
+    # stream as soon as they arrive, beside this rank's row pass (as the
+    # single-process step builds it beside k_row)
+    side = _csr_stream(dev) if FX_CSR_AHEAD else None
+    if FX_CSR_AHEAD:
+        if side is not None:
+            side.wait_stream(torch.cuda.current_stream(dev))  # the previous step's use of the workspace
+            with torch.cuda.stream(side):
+                for h in ids:
+                    h.wait()
+                ops.train_csr(desc, mode, pos_g, neg_g, dev)
+        else:
+            for h in ids:
+                h.wait()
+            ops.train_csr(desc, mode, pos_g, neg_g, dev)
     Le = model.entity_dim
     g_g, dq_g, st_g = _fx_buffers(dev, Bg, n, Le)
     pieces = fx_pieces(B)
@@ -182,6 +212,8 @@ def dp_train_step_factors(model, positive_sample, negative_sample, subsampling_w
             dst.view(world, k, P, *rest).copy_(t.view(k, world, P, *rest).transpose(0, 1))
     for h in ids:
         h.wait()
+    if side is not None:
+        torch.cuda.current_stream(dev).wait_stream(side)
     adam = None
     if optimizer is not None and model.fuse_optimizer and hasattr(optimizer, 'prepare_fused'):
         adam = optimizer.prepare_fused(model.entity_embedding, model.relation_embedding, model._modulus(),
@@ -189,7 +221,8 @@ def dp_train_step_factors(model, positive_sample, negative_sample, subsampling_w
     ge, gr, gm, losses = model._grad_buffers()
     ops.train_step_from_rows(desc, mode, pos_g, neg_g, w_g, wsum, dev, uni_weight=uni, uni_batch=Bg,
                              regularization=float(args.regularization), g_in=g_g, dq_in=dq_g, stats=st_g,
-                             grad_entity=ge, grad_relation=gr, grad_modulus=gm, losses=losses, adam=adam)
+                             grad_entity=ge, grad_relation=gr, grad_modulus=gm, losses=losses, adam=adam,
+                             csr_ready=FX_CSR_AHEAD)
     if model.entity_embedding.requires_grad:
         model.entity_embedding.grad = ge
     if model.relation_embedding.requires_grad:

@@ -250,14 +250,29 @@ def train_rows_slice(desc: _lib.ModelDesc, mode: str, pos: torch.Tensor, neg: to
         "kge_train_rows_slice")
 
 
+def train_csr(desc: _lib.ModelDesc, mode: str, pos: torch.Tensor, neg: torch.Tensor, dev) -> None:
+    """The occurrence CSR of the (gathered) batch into the step workspace
+    (kge_train_csr), ahead of train_step_from_rows(..., csr_ready=True) — it
+    needs only the ids, so it runs while the row factors are on the wire."""
+    if mode not in ("head-batch", "tail-batch"):
+        raise ValueError("Training batch mode %s not supported" % mode)
+    pos, neg = _idx(pos, dev), _idx(neg, dev)
+    B, n = neg.shape
+    ws = _train_ws(desc, B, n, dev)
+    st = state(dev)
+    _lib.check(_lib.load().kge_train_csr(desc, _lib.MODE_IDS[mode], pos.data_ptr(), neg.data_ptr(), B, n,
+                                         ws.data_ptr(), ws.numel(), st.err.data_ptr(), _stream(dev)), "kge_train_csr")
+
+
 def train_step_from_rows(desc: _lib.ModelDesc, mode: str, pos: torch.Tensor, neg: torch.Tensor, sub_w: torch.Tensor,
                          weight_sum_dev: Optional[torch.Tensor], dev, *, uni_weight: bool, uni_batch: int,
                          regularization: float, g_in: torch.Tensor, dq_in: torch.Tensor, stats: torch.Tensor,
                          grad_entity: torch.Tensor, grad_relation: torch.Tensor, grad_modulus: Optional[torch.Tensor],
-                         losses: torch.Tensor, adam: Optional[_lib.AdamDesc] = None) -> None:
+                         losses: torch.Tensor, adam: Optional[_lib.AdamDesc] = None, csr_ready: bool = False) -> None:
     """The rest of the step for the whole (gathered) batch from the exchanged
-    row factors (kge_train_step_from_rows); bit-identical to one process
-    running train_step_grads / the fused step on that batch."""
+    row factors (kge_train_step_from_rows; with csr_ready the CSR train_csr
+    built for this batch, kge_train_step_from_rows_csr); bit-identical to one
+    process running train_step_grads / the fused step on that batch."""
     if mode not in ("head-batch", "tail-batch"):
         raise ValueError("Training batch mode %s not supported" % mode)
     pos, neg = _idx(pos, dev), _idx(neg, dev)
@@ -266,11 +281,12 @@ def train_step_from_rows(desc: _lib.ModelDesc, mode: str, pos: torch.Tensor, neg
     _check_row_buffers(dev, B, n, desc.entity_dim, g_in, dq_in, stats)
     ws = _train_ws(desc, B, n, dev)
     st = state(dev)
-    _lib.check(_lib.load().kge_train_step_from_rows(
+    fn = "kge_train_step_from_rows_csr" if csr_ready else "kge_train_step_from_rows"
+    _lib.check(getattr(_lib.load(), fn)(
         desc, _lib.MODE_IDS[mode], pos.data_ptr(), neg.data_ptr(), B, n, w.data_ptr(), _ptr(weight_sum_dev),
         int(bool(uni_weight)), int(uni_batch), float(regularization), g_in.data_ptr(), dq_in.data_ptr(),
         stats.data_ptr(), adam, grad_entity.data_ptr(), grad_relation.data_ptr(), _ptr(grad_modulus),
-        losses.data_ptr(), ws.data_ptr(), ws.numel(), st.err.data_ptr(), _stream(dev)), "kge_train_step_from_rows")
+        losses.data_ptr(), ws.data_ptr(), ws.numel(), st.err.data_ptr(), _stream(dev)), fn)
 
 
 def adam_step(param: torch.Tensor, grad: torch.Tensor, exp_avg: torch.Tensor, exp_avg_sq: torch.Tensor, *,

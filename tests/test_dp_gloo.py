@@ -152,13 +152,17 @@ def _fx_worker(rank, world, port, uni, out):
         seen["slice"] = (uni_batch, None if wsum is None else float(wsum[0]))
         _fx_rows(pos, neg, w, g_out, dq_out, stats_out)
 
+    def csr(desc, mode, pos, neg, dev):
+        seen["csr"] = [t.clone() for t in (pos, neg)]
+
     def from_rows(desc, mode, pos, neg, w, wsum, dev, *, uni_weight, uni_batch, regularization, g_in, dq_in, stats,
-                  grad_entity, grad_relation, grad_modulus, losses, adam=None):
+                  grad_entity, grad_relation, grad_modulus, losses, adam=None, csr_ready=False):
+        seen["csr_ready"] = csr_ready
         seen["global"] = [t.clone() for t in (pos, neg, w, g_in, dq_in, stats)]
         seen["global_scalars"] = (uni_batch, regularization, None if wsum is None else float(wsum[0]))
         losses.copy_(torch.tensor([float(w.sum()), float(g_in.sum()), float(dq_in.sum()), float(stats.sum()), 0.]))
 
-    ops.train_rows_slice, ops.train_step_from_rows = rows_slice, from_rows
+    ops.train_rows_slice, ops.train_step_from_rows, ops.train_csr = rows_slice, from_rows, csr
     ops.weight_sum = lambda w, o: o.copy_(w.sum().reshape(1))
     model = _make_model("RotatE")
     pos, neg, w = synth.kge_batch(5, B, N, E, R)
@@ -186,6 +190,8 @@ def test_factor_exchange_gathers_global_batch(uni, world):
         for got, want in zip(s["global"], (pos, neg, w, g, dq, st)):
             assert torch.equal(got, want.to(got.dtype))
         assert s["slice"][0] == B and s["global_scalars"][:2] == (B, 1e-3)
+        # the CSR built ahead saw the same global ids the rest of the step sees
+        assert s["csr_ready"] and all(torch.equal(a, b) for a, b in zip(s["csr"], s["global"][:2]))
         if uni:
             assert s["slice"][1] is None and s["global_scalars"][2] is None
         else:  # Σw of the GLOBAL weights, on both sides of the exchange

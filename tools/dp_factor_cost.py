@@ -82,6 +82,16 @@ def main():
                                  temperature=1.0, uni_weight=False, uni_batch=Bg, g_out=g_g[sl], dq_out=dq_g[sl],
                                  stats_out=st_g[sl])
         res[f"global_step_ms_N{world}"] = timed(glob, a.reps)
+
+        def glob_csr():  # the CSR already built (kge_train_csr ran while the factors were on the wire)
+            adam = opt.prepare_fused(m.entity_embedding, m.relation_embedding, None, write_grad=True)
+            ops.train_step_from_rows(desc, "tail-batch", pg, ng, wg, wsum, dev, uni_weight=False, uni_batch=Bg,
+                                     regularization=0.0, g_in=g_g, dq_in=dq_g, stats=st_g, grad_entity=ge,
+                                     grad_relation=gr, grad_modulus=gm, losses=losses, adam=adam, csr_ready=True)
+            opt.step()
+        ops.train_csr(desc, "tail-batch", pg, ng, dev)
+        res[f"global_step_ms_N{world}_csr_ahead"] = timed(glob_csr, a.reps)
+        res[f"csr_ms_N{world}"] = timed(lambda: ops.train_csr(desc, "tail-batch", pg, ng, dev), a.reps)
         res[f"exchange_bytes_per_rank_N{world}"] = (B * Le + B * N + 4 * B) * 4 + B * (N + 3) * 8 + 4 * B
     res["allreduce_bytes_per_rank_grads"] = {f"N{k}": 2 * (k - 1) / k * E * Le * 4 for k in (2, 4, 8)}
     print(json.dumps(res), flush=True)
