@@ -166,17 +166,19 @@ def dp_train_step_factors(model, positive_sample, negative_sample, subsampling_w
     # stream as soon as they arrive, beside this rank's row pass (as the
     # single-process step builds it beside k_row)
     side = _csr_stream(dev) if FX_CSR_AHEAD else None
+    gws = None  # the global step's own workspace (the row pass below uses the shared one meanwhile)
     if FX_CSR_AHEAD:
+        gws = ops.exchange_workspace(desc, Bg, n, dev) if dev.type == "cuda" else None
         if side is not None:
-            side.wait_stream(torch.cuda.current_stream(dev))  # the previous step's use of the workspace
+            side.wait_stream(torch.cuda.current_stream(dev))  # the previous step's use of that workspace
             with torch.cuda.stream(side):
                 for h in ids:
                     h.wait()
-                ops.train_csr(desc, mode, pos_g, neg_g, dev)
+                ops.train_csr(desc, mode, pos_g, neg_g, dev, workspace=gws)
         else:
             for h in ids:
                 h.wait()
-            ops.train_csr(desc, mode, pos_g, neg_g, dev)
+            ops.train_csr(desc, mode, pos_g, neg_g, dev, workspace=gws)
     Le = model.entity_dim
     g_g, dq_g, st_g = _fx_buffers(dev, Bg, n, Le)
     pieces = fx_pieces(B)
@@ -222,7 +224,7 @@ def dp_train_step_factors(model, positive_sample, negative_sample, subsampling_w
     ops.train_step_from_rows(desc, mode, pos_g, neg_g, w_g, wsum, dev, uni_weight=uni, uni_batch=Bg,
                              regularization=float(args.regularization), g_in=g_g, dq_in=dq_g, stats=st_g,
                              grad_entity=ge, grad_relation=gr, grad_modulus=gm, losses=losses, adam=adam,
-                             csr_ready=FX_CSR_AHEAD)
+                             csr_ready=FX_CSR_AHEAD, workspace=gws)
     if model.entity_embedding.requires_grad:
         model.entity_embedding.grad = ge
     if model.relation_embedding.requires_grad:

@@ -220,6 +220,27 @@ def _train_ws(desc: _lib.ModelDesc, B: int, n: int, dev) -> torch.Tensor:
     return state(dev).workspace(need)
 
 
+_AUX_WS: dict = {}
+
+
+def exchange_workspace(desc: _lib.ModelDesc, B: int, n: int, dev) -> torch.Tensor:
+    """A step workspace of its own for the factor exchange's global batch:
+    train_csr runs on a side stream while this rank's row pass (which uses the
+    shared per-device workspace) is still running, so the two must not share
+    memory.  Grown (after a device sync) only when a larger batch comes."""
+    lib = _lib.load()
+    key = (desc.entity_dim, desc.relation_dim, desc.nentity, desc.nrelation, B, n)
+    need = _WS_BYTES.get(key)
+    if need is None:
+        need = _WS_BYTES[key] = lib.kge_train_workspace_bytes(desc, B, n)
+    t = _AUX_WS.get(dev)
+    if t is None or t.numel() < need:
+        if t is not None:
+            torch.cuda.synchronize(dev)  # the old buffer may still be read on either stream
+        t = _AUX_WS[dev] = torch.empty(int(need * 1.25) + 4096, dtype=torch.uint8, device=dev)
+    return t
+
+
 def _check_row_buffers(dev, B: int, n: int, Le: int, g, dq, stats) -> None:
     for t, shape in ((g, (B, n)), (dq, (B, Le)), (stats, (B, 4))):
         if (tuple(t.shape) != shape or not t.is_contiguous() or t.dtype != torch.float32
@@ -250,15 +271,17 @@ def train_rows_slice(desc: _lib.ModelDesc, mode: str, pos: torch.Tensor, neg: to
         "kge_train_rows_slice")
 
 
-def train_csr(desc: _lib.ModelDesc, mode: str, pos: torch.Tensor, neg: torch.Tensor, dev) -> None:
-    """The occurrence CSR of the (gathered) batch into the step workspace
-    (kge_train_csr), ahead of train_step_from_rows(..., csr_ready=True) — it
-    needs only the ids, so it runs while the row factors are on the wire."""
+def train_csr(desc: _lib.ModelDesc, mode: str, pos: torch.Tensor, neg: torch.Tensor, dev,
+              workspace: Optional[torch.Tensor] = None) -> None:
+    """The occurrence CSR of the (gathered) batch into a step workspace
+    (kge_train_csr), ahead of train_step_from_rows(..., csr_ready=True) with
+    the SAME workspace — it needs only the ids, so it runs while the row
+    factors are on the wire."""
     if mode not in ("head-batch", "tail-batch"):
         raise ValueError("Training batch mode %s not supported" % mode)
     pos, neg = _idx(pos, dev), _idx(neg, dev)
     B, n = neg.shape
-    ws = _train_ws(desc, B, n, dev)
+    ws = workspace if workspace is not None else _train_ws(desc, B, n, dev)
     st = state(dev)
     _lib.check(_lib.load().kge_train_csr(desc, _lib.MODE_IDS[mode], pos.data_ptr(), neg.data_ptr(), B, n,
                                          ws.data_ptr(), ws.numel(), st.err.data_ptr(), _stream(dev)), "kge_train_csr")
@@ -268,7 +291,8 @@ def train_step_from_rows(desc: _lib.ModelDesc, mode: str, pos: torch.Tensor, neg
                          weight_sum_dev: Optional[torch.Tensor], dev, *, uni_weight: bool, uni_batch: int,
                          regularization: float, g_in: torch.Tensor, dq_in: torch.Tensor, stats: torch.Tensor,
                          grad_entity: torch.Tensor, grad_relation: torch.Tensor, grad_modulus: Optional[torch.Tensor],
-                         losses: torch.Tensor, adam: Optional[_lib.AdamDesc] = None, csr_ready: bool = False) -> None:
+                         losses: torch.Tensor, adam: Optional[_lib.AdamDesc] = None, csr_ready: bool = False,
+                         workspace: Optional[torch.Tensor] = None) -> None:
     """The rest of the step for the whole (gathered) batch from the exchanged
     row factors (kge_train_step_from_rows; with csr_ready the CSR train_csr
     built for this batch, kge_train_step_from_rows_csr); bit-identical to one
@@ -279,7 +303,7 @@ def train_step_from_rows(desc: _lib.ModelDesc, mode: str, pos: torch.Tensor, neg
     w = sub_w.to(dev, dtype=torch.float32).contiguous().view(-1)
     B, n = neg.shape
     _check_row_buffers(dev, B, n, desc.entity_dim, g_in, dq_in, stats)
-    ws = _train_ws(desc, B, n, dev)
+    ws = workspace if workspace is not None else _train_ws(desc, B, n, dev)
     st = state(dev)
     fn = "kge_train_step_from_rows_csr" if csr_ready else "kge_train_step_from_rows"
     _lib.check(getattr(_lib.load(), fn)(

@@ -152,11 +152,11 @@ def _fx_worker(rank, world, port, uni, out):
         seen["slice"] = (uni_batch, None if wsum is None else float(wsum[0]))
         _fx_rows(pos, neg, w, g_out, dq_out, stats_out)
 
-    def csr(desc, mode, pos, neg, dev):
+    def csr(desc, mode, pos, neg, dev, workspace=None):
         seen["csr"] = [t.clone() for t in (pos, neg)]
 
     def from_rows(desc, mode, pos, neg, w, wsum, dev, *, uni_weight, uni_batch, regularization, g_in, dq_in, stats,
-                  grad_entity, grad_relation, grad_modulus, losses, adam=None, csr_ready=False):
+                  grad_entity, grad_relation, grad_modulus, losses, adam=None, csr_ready=False, workspace=None):
         seen["csr_ready"] = csr_ready
         seen["global"] = [t.clone() for t in (pos, neg, w, g_in, dq_in, stats)]
         seen["global_scalars"] = (uni_batch, regularization, None if wsum is None else float(wsum[0]))
