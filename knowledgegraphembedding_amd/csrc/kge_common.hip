@@ -67,6 +67,29 @@ __global__ __launch_bounds__(256) void k_csr_rank(CsrArgs a) {
   }
 }
 
+// The same ranks with one wave per bucket: the bucket's ids are read once,
+// 64 at a time, and each lane counts the smaller ids by broadcasting the
+// others' lane by lane (readlane) — ⌈m/64⌉²·64 register steps per bucket
+// instead of m global reads per id, which matters once buckets hold
+// hundreds of ids (the factor exchange's global batch).  Same output.
+__global__ __launch_bounds__(256) void k_csr_rank_w(CsrArgs a, int64_t nb) {
+  const int lane = threadIdx.x & 63;
+  const int64_t b = (int64_t)blockIdx.x * 4 + wave_id();
+  if (b >= nb) return;
+  const int32_t b0 = a.off[b], b1 = a.off[b + 1];
+  for (int32_t c0 = b0; c0 < b1; c0 += 64) {
+    const bool mine = c0 + lane < b1;
+    const int32_t v = mine ? a.tmp[c0 + lane] : 0x7fffffff;
+    int32_t r = 0;
+    for (int32_t d0 = b0; d0 < b1; d0 += 64) {
+      const int32_t o = (d0 + lane < b1) ? a.tmp[d0 + lane] : 0x7fffffff;
+      const int cnt = (b1 - d0 < 64) ? (b1 - d0) : 64;
+      for (int l = 0; l < cnt; ++l) r += (__builtin_amdgcn_readlane(o, l) < v) ? 1 : 0;
+    }
+    if (mine) a.occ[b0 + r] = v;
+  }
+}
+
 __global__ __launch_bounds__(256) void k_rel_rows(RelArgs a) {
   const int lane = threadIdx.x & 63;
   const int64_t rr = (int64_t)blockIdx.x * 4 + wave_id();
@@ -261,7 +284,11 @@ int launch_csr(const CsrArgs& a, hipStream_t s) {
   e = rocprim::exclusive_scan(a.scan_tmp, bytes, a.cnt, a.off, int32_t(0), (size_t)nb + 1, rocprim::plus<int32_t>(), s);
   if (e != hipSuccess) return (int)e;
   hipLaunchKernelGGL(k_csr_fill, dim3(grid_for(N)), dim3(256), 0, s, a);
-  hipLaunchKernelGGL(k_csr_rank, dim3(grid_for(N)), dim3(256), 0, s, a);
+  // bucket-per-wave ranks (KGE_CSR_RANK=1, default) or id-per-thread (0): same output
+  if (env_int_c("KGE_CSR_RANK", 1) == 1)
+    hipLaunchKernelGGL(k_csr_rank_w, dim3((unsigned)((nb + 3) / 4)), dim3(256), 0, s, a, nb);
+  else
+    hipLaunchKernelGGL(k_csr_rank, dim3(grid_for(N)), dim3(256), 0, s, a);
   return (int)hipGetLastError();
 }
 
