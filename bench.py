@@ -14,14 +14,19 @@ batches pre-staged in HBM (the CPU sampler cannot feed this rate; SURVEY §7 v)
 and alternating tail-/head-batch like BidirectionalOneShotIterator.
 Data: synthetic (uniform ids, reference init U(-range, range) tables).
 
-`--workload yago3-10-rowpart` runs BASELINE config 5 instead: RotatE YAGO3-10
-shape (E=123182, R=37) d=1000 -de, b=1024 per GPU, n=1024, with the entity
-table row-partitioned across the ranks (partition.py: reduce-scatter of the
-dense entity gradient to the row owners, shard Adam, all-gather of the rows).
+`--workload fb15k-237` runs BASELINE config 4's shape: RotatE FB15k-237
+(E=14541, R=237) d=1000 -de, b=1024 per GPU (global 8192 on 8 GPUs), n=256,
+data-parallel.  `--workload yago3-10-rowpart` runs BASELINE config 5: RotatE
+YAGO3-10 shape (E=123182, R=37) d=1000 -de, b=1024 per GPU, n=1024, with the
+entity table row-partitioned across the ranks (partition.py: reduce-scatter of
+the dense entity gradient to the row owners, shard Adam, all-gather of the rows).
 
 Prints one JSON line (rank 0).  `roofline` is the dominant kernel (the fused
-row pass) timed live with HIP events on its launch stream; `cpu_baseline` is
-the oracle's ATen op chain (the reference's algorithm) on this host.
+row pass) timed live with HIP events on its launch stream, `roofline_entity`
+the entity pass the same way; `step_roofline` sums both kernels' bytes over the
+whole step time.  `traffic` fields are rocprofv3 PMC bytes per launch from the
+committed profiles/ summaries.  `cpu_baseline` is the oracle's ATen op chain
+(the reference's algorithm) on this host.
 """
 from __future__ import annotations
 
@@ -46,6 +51,9 @@ WORKLOADS = {
     # BASELINE config 2 (the headline metric; the driver's default)
     "fb15k": dict(E=14951, R=1345, D=1000, B=1024, NNEG=256, partition=False,
                   name="RotatE FB15k-shape train_step (fused score+self-adv loss+bwd, dense Adam)"),
+    # BASELINE config 4 (FB15k-237 shape, 1024 per rank; the 8-GPU driver run makes global 8192)
+    "fb15k-237": dict(E=14541, R=237, D=1000, B=1024, NNEG=256, partition=False,
+                      name="RotatE FB15k-237-shape train_step, data-parallel (fused score+self-adv loss+bwd, dense Adam)"),
     # BASELINE config 5
     "yago3-10-rowpart": dict(E=123182, R=37, D=1000, B=1024, NNEG=1024, partition=True,
                              name="RotatE YAGO3-10-shape train_step, entity rows partitioned over the ranks "
@@ -55,36 +63,55 @@ TIMER_PERIOD = 8
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
 
 
-def algorithmic_row_bytes(b: int, n: int, le: int, lr: int, fused_tail: bool = True) -> int:
-    """Bytes one fused row-pass launch must move.  Reads: every
-    negative row once, the positive h/r/t rows, indices and weights.  Writes:
-    dL/ds [b, n], q [b, le] for the entity pass, the row statistics, and — with
-    the epilogue fused into the launch (the default) — the head/tail [2b, le]
-    and relation [b, lr] gradient contributions (else dL/dq [b, le])."""
+def algorithmic_row_bytes(b: int, n: int, le: int, lr: int) -> int:
+    """Bytes one fused row-pass launch (k_row) must move.  Reads:
+    every negative row once, the positive h/r/t rows, indices and weights.
+    Writes: dL/ds [b, n], q [b, le] for the entity pass, the row statistics, and
+    (the epilogue is fused into the launch) the head/tail [2b, le] and relation
+    [b, lr] gradient contributions."""
     reads = b * n * le * 4 + b * (le + lr + le) * 4 + b * n * 8 + b * 3 * 8 + b * 4
-    writes = b * n * 4 + b * le * 4 + b * 16 + ((2 * b * le + b * lr) * 4 if fused_tail else b * le * 4)
+    writes = b * n * 4 + b * le * 4 + b * 16 + (2 * b * le + b * lr) * 4
     return reads + writes
 
 
-def step_roofline(step_s: float) -> dict:
-    """Whole-step HBM roofline: the bytes any fwd+bwd implementation must move
-    (read every negative/positive row, indices, weights; write each touched
-    gradient row once) and, separately, + a dense Adam over both tables
-    (param/grad/m/v read, param/m/v written = 28 B per element)."""
-    le, lr = 2 * D, D
-    fwd = B * NNEG * le * 4 + B * (le + lr + le) * 4 + B * NNEG * 8 + B * 3 * 8 + B * 4
-    fwd_bwd = fwd + B * (NNEG + 2) * le * 4 + B * lr * 4
-    adam = 28 * (E * le + R * lr)
+def algorithmic_entity_bytes(e: int, r: int, b: int, n: int, le: int, lr: int) -> int:
+    """Bytes the entity pass (k_entity_sl with the relation rows in its
+    trailing blocks, Adam fused) must move: per table element the fused Adam
+    stream reads param, exp_avg, exp_avg_sq and writes them back plus the dense
+    gradient (28 B); plus one read of every input it gathers — q [b, le], the
+    row contributions [2b, le] and [b, lr], dL/ds [b, n], the occurrence CSR
+    (ids + offsets).  The q rows are gathered once per occurrence from L2; only
+    their first touch is counted here."""
+    adam = 28 * (e * le + r * lr)
+    inputs = b * le * 4 + (2 * b * le + b * lr) * 4 + b * n * 4 + (b * n + 3 * b) * 4 + (e + r + 1) * 4
+    return adam + inputs
 
+
+def step_roofline(step_s: float, row_bytes: int, ent_bytes: int, row_traffic, ent_traffic) -> dict:
+    """Whole-step view: the two kernels' algorithmic bytes (and their PMC bytes
+    when a committed summary exists) over the measured step time.  Every
+    figure counts each byte once, so no fraction can exceed 1 unless the
+    kernels beat the HBM peak."""
     def gbs(nbytes):
         return nbytes / step_s / 1e9
 
-    return {"algorithmic_bytes_fwd_bwd": fwd_bwd, "achieved_fwd_bwd": gbs(fwd_bwd),
-            "frac_fwd_bwd": gbs(fwd_bwd) / HBM_PEAK_GBS,
-            "algorithmic_bytes_with_adam": fwd_bwd + adam, "achieved_with_adam": gbs(fwd_bwd + adam),
-            "frac_with_adam": gbs(fwd_bwd + adam) / HBM_PEAK_GBS, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "note": "algorithmic bytes / measured step time; the FB15k tables (120 MB) and part of the Adam "
-                    "state stay in the 256 MB Infinity Cache, so a fraction above 1 is fabric-side, not HBM"}
+    alg = row_bytes + ent_bytes
+    out = {"algorithmic_bytes": alg, "achieved": gbs(alg), "frac": gbs(alg) / HBM_PEAK_GBS,
+           "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "what": "k_row + entity pass algorithmic bytes / measured step time (includes launch gaps, CSR join, "
+                   "finalize and the loss read-back)"}
+    if row_traffic and ent_traffic:
+        tr = row_traffic + ent_traffic
+        out.update({"traffic": tr, "achieved_traffic": gbs(tr), "frac_traffic": gbs(tr) / HBM_PEAK_GBS})
+    return out
+
+
+def _pmc_bytes(path: str):
+    """hbm_bytes_per_launch from a committed tools/pmc_traffic.py summary."""
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        return json.load(f).get("hbm_bytes_per_launch")
 
 
 class DeviceBatches:
@@ -114,11 +141,29 @@ class DeviceBatches:
         return pos, neg, w, ('head-batch' if self.step % 2 == 0 else 'tail-batch')
 
 
+def _cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(model_cpu_state, budget_s: float = 12.0, b: int = 32):
     """The oracle (reference op chain on CPU fp32, + torch.optim.Adam) on a
-    bounded sample of the same workload: b positives x 256 negatives."""
+    bounded sample of the same workload: b positives x 256 negatives, on every
+    host core this process may run on.  The per-triple rate grows a little
+    with b: measured in the build container on 8 cores, b = 32 gives 3.9 k and
+    b = 1024 5.0 k triples/s (profiles/r02/cpu_baseline_bscaling.json), so the
+    bounded b = 32 sample understates the full-batch CPU rate by about 1.26x;
+    the line carries that ratio next to the sample."""
     from oracle import kge_oracle as O
     ent, rel, erange = model_cpu_state
+    cores = len(os.sched_getaffinity(0))
+    torch.set_num_threads(cores)
     g = torch.Generator().manual_seed(7)
     pos = torch.stack([torch.randint(0, E, (b,), generator=g), torch.randint(0, R, (b,), generator=g),
                        torch.randint(0, E, (b,), generator=g)], 1)
@@ -144,10 +189,12 @@ def cpu_baseline(model_cpu_state, budget_s: float = 12.0, b: int = 32):
         if time.perf_counter() - t0 > budget_s or k >= 16:
             break
     dt = time.perf_counter() - t0
-    return {"value": k * b * (NNEG + 1) / dt, "unit": "triples/s", "cores": torch.get_num_threads(),
-            "kind": "port",
+    return {"value": k * b * (NNEG + 1) / dt, "unit": "triples/s", "cores": cores, "cpu_model": _cpu_model(),
+            "kind": "port", "b1024_over_b32_rate": 1.264,
+            "b_scaling_source": "profiles/r02/cpu_baseline_bscaling.json (build container, 8 cores)",
             "sample": f"oracle train step (ATen op chain fwd + autograd bwd + torch Adam), RotatE E={E} R={R} "
-                      f"d={D} b={b} n={NNEG} adv, {k} timed steps after 1 warm-up, {dt:.1f} s"}
+                      f"d={D} b={b} n={NNEG} adv, {k} timed steps after 1 warm-up, {dt:.1f} s, "
+                      f"torch threads = {cores}"}
 
 
 def main():
@@ -242,17 +289,20 @@ def main():
         dt = float(t.item())
 
     calls = max(1.0, float(stage[6]))
+    here = os.path.dirname(os.path.abspath(__file__))
     row_ms = float(stage[1]) / calls
-    row_bytes = algorithmic_row_bytes(B, NNEG, 2 * D, D, fused_tail=os.environ.get("KGE_FUSE_EPI", "1") != "0")
+    ent_ms = float(stage[4]) / calls
+    row_bytes = algorithmic_row_bytes(B, NNEG, 2 * D, D)
+    ent_bytes = algorithmic_entity_bytes(E, R, B, NNEG, 2 * D, D)
     achieved = row_bytes / (row_ms * 1e-3) / 1e9 if row_ms > 0 else None
-    traffic = None
-    tj = a.traffic_json or os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "pmc_traffic.json")
-    if a.workload == "fb15k" and os.path.exists(tj):
-        with open(tj) as f:
-            traffic = json.load(f).get("hbm_bytes_per_launch")
+    ent_achieved = ent_bytes / (ent_ms * 1e-3) / 1e9 if ent_ms > 0 else None
+    row_traffic = ent_traffic = None
+    if a.workload == "fb15k":  # PMC summaries of this workload (tools/profile.sh + tools/pmc_traffic.py)
+        row_traffic = _pmc_bytes(a.traffic_json or os.path.join(here, "profiles", "pmc_traffic.json"))
+        ent_traffic = _pmc_bytes(os.path.join(here, "profiles", "pmc_traffic_entity.json"))
 
     ceiling = None  # k_row's access pattern alone (tools/dbg/gather_ceiling.hip), measured on MI355X
-    cj = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r01", "gather_ceiling.jsonl")
+    cj = os.path.join(here, "profiles", "r01", "gather_ceiling.jsonl")
     if a.workload == "fb15k" and os.path.exists(cj) and achieved:
         with open(cj) as f:
             c0 = json.loads(f.readline())
@@ -273,26 +323,34 @@ def main():
         "vs_baseline": None,
         "dtype": "fp32",
         "data": "synthetic (uniform ids, U(-range,range) tables), batches pre-staged in HBM",
-        "variant": {"fused_adam": model.fuse_optimizer, "keep_grads": model.keep_grads,
-                    "row_pipe": os.environ.get("KGE_ROW_PIPE", "0"), "batches": sampler,
+        "variant": {"fused_adam": model.fuse_optimizer, "keep_grads": model.keep_grads, "batches": sampler,
                     "dp_exchange": (None if group is None or part is not None else dp_exchange_mode(world))},
         "config": {"workload": wl["name"],
                    "entities": E, "relations": R, "hidden_dim": D, "batch_per_gpu": B, "global_batch": B * world,
                    "negatives": NNEG, "adversarial_temperature": TEMP, "gamma": GAMMA,
                    "parallelism": (f"rowpart{world}" if part is not None else f"dp{world}")},
         "stage_timed_steps": int(stage[6]),
-        "stage_ms": {"build_q": float(stage[0]) / calls, "row_pass": row_ms, "row_epilogue": float(stage[2]) / calls,
-                     "csr_join": float(stage[3]) / calls, "entity_pass": float(stage[4]) / calls,
-                     "relation_join_finalize": float(stage[5]) / calls,
-                     "other_incl_adam_ms": dt / a.steps * 1e3 - float(stage[:6].sum()) / calls},
+        # HIP-event stage times of one step in TIMER_PERIOD, on the launching
+        # stream; the CSR runs on a side stream beside the row pass, so these
+        # are not a decomposition of ms_per_step
+        "stage_ms": {"row_pass": row_ms, "csr_join": float(stage[3]) / calls, "entity_pass": ent_ms,
+                     "relation_join_finalize": float(stage[5]) / calls},
         "roofline": {"bound": "hbm", "kernel": "k_row (q build + negative scoring + self-adversarial loss + q-side backward + positive epilogue)",
                      "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS if achieved else None,
-                     "traffic": traffic, "algorithmic_bytes_per_launch": row_bytes,
+                     "traffic": row_traffic, "algorithmic_bytes_per_launch": row_bytes,
                      "avg_launch_ms": row_ms, "pattern_ceiling": ceiling},
-        "step_roofline": step_roofline(dt / a.steps),
+        "roofline_entity": {"bound": "hbm", "kernel": "k_entity_sl (entity-major gradient + fused Adam; relation rows in trailing blocks)",
+                            "achieved": ent_achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                            "frac": ent_achieved / HBM_PEAK_GBS if ent_achieved else None, "traffic": ent_traffic,
+                            "algorithmic_bytes_per_launch": ent_bytes, "avg_launch_ms": ent_ms},
+        "step_roofline": step_roofline(dt / a.steps, row_bytes, ent_bytes, row_traffic, ent_traffic),
     }
     if a.workload != "fb15k":
         out["metric"] = f"scored (pos+neg) triples/sec, RotatE {a.workload} d={D} b={B} n={NNEG}"
+    fr = [x for x in (out["roofline"]["frac"], out["roofline_entity"]["frac"], out["step_roofline"]["frac"],
+                      out["step_roofline"].get("frac_traffic")) if x is not None]
+    if any(f > 1.0 for f in fr):
+        print(f"bench.py: a roofline fraction exceeds 1 ({fr}); the byte model is wrong", file=sys.stderr)
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(cpu_state, budget_s=a.cpu_budget)
     if rank == 0:

@@ -107,26 +107,9 @@ struct Carver {
 struct GradWs {
   float *g, *q, *dq, *ent_contrib, *rel_contrib, *row_stats, *reg_partial, *wsum;
   int32_t *keys, *cnt, *off, *tmp, *occ;
-  int2* meta;
   void* scan_tmp;
   size_t scan_tmp_bytes;
 };
-
-// Column tiles of the LDS-tiled entity pass (k_entity_tl): 16 complex dims
-// or 32 real dims per tile.
-int ent_tiles(const kge_model_desc* m) {
-  const bool cplx = (m->model == KGE_COMPLEX || m->model == KGE_ROTATE);
-  return cplx ? (m->entity_dim / 2 + 15) / 16 : (m->entity_dim + TL_COLS - 1) / TL_COLS;
-}
-int device_cus() {
-  static int n = [] {
-    int dev = 0, v = 0;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0)
-      v = 256;
-    return v;
-  }();
-  return n;
-}
 
 GradWs carve_grad(void* ws, const kge_model_desc* m, int64_t B, int64_t n, size_t* bytes) {
   Carver c(ws);
@@ -138,15 +121,13 @@ GradWs carve_grad(void* ws, const kge_model_desc* m, int64_t B, int64_t n, size_
   w.ent_contrib = c.take<float>(2 * B * (int64_t)m->entity_dim);
   w.rel_contrib = c.take<float>(B * (int64_t)m->relation_dim);
   w.row_stats = c.take<float>(B * 4);
-  const int64_t parts = ent_tiles(m) > 8 ? ent_tiles(m) : 8;
-  w.reg_partial = c.take<float>(parts * m->nentity + m->nrelation);  // per (entity, column slice/tile) + per relation
+  w.reg_partial = c.take<float>(8 * m->nentity + m->nrelation);  // per (entity, column slice) + per relation
   w.wsum = c.take<float>(4);
   w.keys = c.take<int32_t>(N);
   w.cnt = c.take<int32_t>(nb + 1);
   w.off = c.take<int32_t>(nb + 1);
   w.tmp = c.take<int32_t>(N);
   w.occ = c.take<int32_t>(N);
-  w.meta = c.take<int2>(Bn + 2 * B);  // entity buckets only
   w.scan_tmp_bytes = csr_scan_temp_bytes(nb);
   w.scan_tmp = c.take<uint8_t>((int64_t)w.scan_tmp_bytes);
   *bytes = c.off + 256;
@@ -192,20 +173,7 @@ int env_int(const char* name, int dflt) {
   return e ? atoi(e) : dflt;
 }
 
-// Launch-schedule variants (measured in DESIGN.md; defaults are the fastest):
-//   KGE_SIDE_STREAM=0  everything on the caller's stream (no cross-stream events)
-//   KGE_REL_MAIN=1     relation pass on the caller's stream after the entity pass
-//   KGE_CSR_JOIN=1     join the CSR before the epilogue instead of before the entity pass
-struct Schedule {
-  int side, rel_main, csr_join_early;
-};
-const Schedule& schedule() {
-  static const Schedule sch = {env_int("KGE_SIDE_STREAM", 1), env_int("KGE_REL_MAIN", 0), env_int("KGE_CSR_JOIN", 0)};
-  return sch;
-}
-
 Side* side_for_device() {
-  if (!schedule().side) return nullptr;
   static Side sides[64];
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
@@ -249,7 +217,7 @@ int run_grad(const kge_model_desc* m, const Geom& geo, int mode, const int64_t* 
   const int write_grad = (!adam || adam->write_grad) ? 1 : 0;
   const Consts c = consts_of(m);
   const int Le = m->entity_dim, Lr = m->relation_dim;
-  const size_t lds = sizeof(float) * (2 * 64 * (size_t)geo.ns * geo.vec + (size_t)vb_floats(Le, 64 * geo.ns * geo.vec) + (size_t)ra.n_lds + 32);
+  const size_t lds = sizeof(float) * (2 * 64 * (size_t)geo.ns * geo.vec + (size_t)vb_floats(Le) + (size_t)ra.n_lds + 32);
   if (lds > 64 * 1024) return KGE_ERR_DIM;
   const bool all = (phases == KGE_PHASE_ALL);
   if (e_end < 0) e_end = m->nentity;
@@ -264,8 +232,6 @@ int run_grad(const kge_model_desc* m, const Geom& geo, int mode, const int64_t* 
   Side* sd = side_for_device();
   hipStream_t ss = sd ? sd->s : s;
   int st;
-
-  const Schedule& sch = schedule();
 
   // entity pass variant: column slices (k_entity_sl) when the row fits one
   // 16-B slot per lane per slice; KGE_ENT_SLICES=0 selects the row-per-wave pass
@@ -289,18 +255,12 @@ int run_grad(const kge_model_desc* m, const Geom& geo, int mode, const int64_t* 
       if ((k == 1 || k == 2 || k == 4 || k == 8) && fits(k)) nsl = k;
     }
   }
-  // LDS-tiled entity pass (KGE_ENT_TILE=1, when the batch's q column tile fits
-  // in LDS): bit-identical, but measured slower than the sliced pass on the
-  // FB15k shape (0.34 vs 0.24 ms: 1.6x the VALU work — one complex dim per
-  // lane and 4-entity lockstep — outweighs the L2 gathers it removes)
-  int ntiles = 0;
-  if (env_int("KGE_ENT_TILE", 0) != 0 && B <= TL_MAX_ROWS) ntiles = ent_tiles(m);
-  const int64_t ent_parts = m->nentity * (int64_t)(ntiles > 0 ? ntiles : (nsl > 0 ? nsl : 1));
+  const int64_t ent_parts = m->nentity * (int64_t)(nsl > 0 ? nsl : 1);
   // relation pass: as trailing blocks of the sliced entity launch (one call,
   // no stream join); else beside the entity pass on the side stream (always
-  // so in phased calls), or on the caller's stream
-  const bool rel_fused = all && (nsl > 0 || ntiles > 0) && env_int("KGE_REL_FUSED", 1) != 0;
-  const bool rel_side = sd && !rel_fused && (!sch.rel_main || !all);
+  // so in phased calls)
+  const bool rel_fused = all && nsl > 0;
+  const bool rel_side = sd && !rel_fused;
   RelArgs rl;
   rl.rel = m->relation_embedding; rl.R = m->nrelation; rl.E = m->nentity; rl.B = B; rl.Bn = B * n; rl.Lr = Lr;
   rl.off = w.off; rl.occ = w.occ; rl.rel_contrib = w.rel_contrib; rl.reg3 = 3.f * reg;
@@ -349,7 +309,6 @@ int run_grad(const kge_model_desc* m, const Geom& geo, int mode, const int64_t* 
     if (sd) hipEventRecord(sd->csr_done, ss);
   }
 
-  if (sd && sch.csr_join_early && all && !csr_ready) hipStreamWaitEvent(s, sd->csr_done, 0);
   // epilogue (positive score, chain rule)
   st = launch_status(op.row(mode, geo.vec, geo.ns, 1, ra, lds, s));
   if (st) return st;
@@ -371,7 +330,7 @@ int run_grad(const kge_model_desc* m, const Geom& geo, int mode, const int64_t* 
   }  // KGE_PHASE_ROWS
 
   if (phases & KGE_PHASE_ENTITY) {
-  if (sd && !(all && sch.csr_join_early) && !csr_ready)
+  if (sd && !csr_ready)
     hipStreamWaitEvent(s, sd->csr_done, 0);  // join 1: the entity pass reads the CSR
   if (timed) g_timer.mark(s);
 
@@ -383,38 +342,13 @@ int run_grad(const kge_model_desc* m, const Geom& geo, int mode, const int64_t* 
   ea.q = w.q; ea.ent_contrib = w.ent_contrib; ea.reg3 = 3.f * reg; ea.reg_partial = w.reg_partial;
   ea.grad_ent = grad_entity;
   ea.write_grad = write_grad;
-  static const int ent_minw = [] {
-    const char* e = getenv("KGE_ENT_MINW");
-    return e ? atoi(e) : 3;  // measured: 4 waves/SIMD spills and runs slower
-  }();
-  ea.minw = ent_minw;
   ea.nsl = nsl;
-  // SL_NT: 4 rows in flight, Adam moments up front, packed RotatE math, non-temporal
-  // row/Adam/gradient stream (measured best: entity pass 0.29 → 0.24 ms; SL_PACKED = same with
-  // plain loads/stores).  Read per call (tests switch it).
-  ea.slv = nsl > 0 ? env_int("KGE_ENT_PF", SL_NT) : SL_NT;
   ea.slice_w = nsl > 0 ? (geo.eg.S + nsl - 1) / nsl : 0;
   ea.adam = adam_t(adam ? &adam->entity : nullptr);
   ea.adamk = ak;
   ea.rel = rl;
   ea.B = B;
-  ea.ntiles = ntiles;
-  ea.ngroups = 0;
-  if (ntiles > 0) {  // about one workgroup per CU (each holds ~B*136 B of LDS)
-    const int cus = device_cus();
-    ea.ngroups = (cus + ntiles / 2) / ntiles;
-    if (ea.ngroups < 1) ea.ngroups = 1;
-  }
-  const int rows_per_rel_block = ntiles > 0 ? TL_THREADS / 64 : 4;
-  ea.rel_blocks = rel_fused ? (m->nrelation + rows_per_rel_block - 1) / rows_per_rel_block : 0;
-  ea.meta = w.meta;
-  if (ntiles > 0 && e_end > e_begin) {
-    MetaArgs ma;
-    ma.off = w.off; ma.occ = w.occ; ma.g = ea.g; ma.e_begin = e_begin; ma.e_end = e_end;
-    ma.Bn = B * n; ma.n = n; ma.N = B * n + 2 * B; ma.meta = w.meta;
-    st = launch_status(launch_occ_meta(ma, s));
-    if (st) return st;
-  }
+  ea.rel_blocks = rel_fused ? (m->nrelation + 3) / 4 : 0;
   if (e_end > e_begin) {
     st = launch_status(op.entity(mode, geo.vec, geo.ns, ea, s));
     if (st) return st;
@@ -454,9 +388,7 @@ RowArgs row_args(const kge_model_desc* m, const Geom& geo, const int64_t* pos, c
   ra.Le = m->entity_dim; ra.Lr = m->relation_dim; ra.eg = geo.eg; ra.c = consts_of(m);
   ra.g_out = w.g; ra.q_out = w.q; ra.dq_out = w.dq; ra.ent_contrib = w.ent_contrib; ra.rel_contrib = w.rel_contrib;
   ra.row_stats = w.row_stats; ra.err = err;
-  ra.pipe = env_int("KGE_ROW_PIPE", 0);  // read per call (tests switch it)
-  ra.fuse_q = env_int("KGE_FUSE_Q", 1);  // measured +1.8 %; bit-identical to the separate k_build_q
-  ra.fuse_epi = env_int("KGE_FUSE_EPI", 1);  // measured +1 % once k_row's RotatE math went to register pairs (no spills)
+  ra.fuse_epi = 1;  // measured +1 % over the separate k_row_epi launch
   return ra;
 }
 

@@ -37,18 +37,6 @@ struct FinArgs {
   AdamK adamk;
 };
 
-// Per-occurrence metadata of the entity buckets for the LDS-tiled entity
-// pass: meta[c] = (q row, dL/ds bits) of CSR entry c in [off[e_begin],
-// off[e_end]), or (-1, 0) for a positive-row contribution.
-struct MetaArgs {
-  const int32_t* off;
-  const int32_t* occ;
-  const float* g;
-  int64_t e_begin, e_end, Bn, n, N;
-  int2* meta;
-};
-int launch_occ_meta(const MetaArgs& a, hipStream_t s);
-
 int launch_rank_mfma(const float* q, const float* ent, int64_t nq, int64_t E, int K, const int64_t* true_id,
                      float* s_true, const int64_t* filt_off, const int64_t* filt_ids, uint32_t* bits, int32_t* gt,
                      int32_t* eq, int64_t* ranks, int32_t* ties, int32_t* err, hipStream_t s);

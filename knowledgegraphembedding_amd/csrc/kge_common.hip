@@ -54,24 +54,11 @@ __global__ __launch_bounds__(256) void k_csr_fill(CsrArgs a) {
 
 // Deterministic order: each id's final slot is its rank among the ids of its
 // bucket (ids are unique), so buckets come out ascending whatever order the
-// atomics filled them in.
-__global__ __launch_bounds__(256) void k_csr_rank(CsrArgs a) {
-  const int64_t N = a.Bn + 3 * a.B;
-  for (int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x; k < N; k += (int64_t)gridDim.x * 256) {
-    const int32_t key = a.keys[k];
-    if (key < 0) continue;
-    const int32_t b0 = a.off[key], b1 = a.off[key + 1];
-    int32_t r = 0;
-    for (int32_t p = b0; p < b1; ++p) r += (a.tmp[p] < (int32_t)k);
-    a.occ[b0 + r] = (int32_t)k;
-  }
-}
-
-// The same ranks with one wave per bucket: the bucket's ids are read once,
+// atomics filled them in.  One wave per bucket: the bucket's ids are read once,
 // 64 at a time, and each lane counts the smaller ids by broadcasting the
 // others' lane by lane (readlane) — ⌈m/64⌉²·64 register steps per bucket
 // instead of m global reads per id, which matters once buckets hold
-// hundreds of ids (the factor exchange's global batch).  Same output.
+// hundreds of ids (the factor exchange's global batch).
 __global__ __launch_bounds__(256) void k_csr_rank_w(CsrArgs a, int64_t nb) {
   const int lane = threadIdx.x & 63;
   const int64_t b = (int64_t)blockIdx.x * 4 + wave_id();
@@ -233,11 +220,6 @@ __global__ __launch_bounds__(256) void k_adam(float* __restrict__ p, const float
 }
 
 // ------------------------------------------------------------ launchers
-static int env_int_c(const char* name, int dflt) {  // read per call (A/B knobs)
-  const char* e = getenv(name);
-  return e ? atoi(e) : dflt;
-}
-
 static inline unsigned grid_for(int64_t n, unsigned cap = 4096) {
   int64_t g = (n + 255) / 256;
   if (g < 1) g = 1;
@@ -247,20 +229,6 @@ static inline unsigned grid_for(int64_t n, unsigned cap = 4096) {
 // Bucket offsets: a device-wide exclusive scan of cnt[0..nb] (cnt[nb] = 0, so
 // off[nb] = total) — rocPRIM's decoupled look-back scan, integer and exact;
 // its scratch comes from the caller's workspace.
-// One thread per CSR entry of the chunk's entity buckets.
-__global__ __launch_bounds__(256) void k_occ_meta(MetaArgs a) {
-  const int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  const int32_t lo = a.off[a.e_begin], hi = a.off[a.e_end];
-  if (c < lo || c >= hi) return;
-  const int32_t o = a.occ[c];
-  int2 m = make_int2(-1, 0);
-  if (o < a.Bn) {
-    m.x = (int32_t)((uint32_t)o / (uint32_t)a.n);
-    m.y = __float_as_int(a.g[o]);
-  }
-  a.meta[c] = m;
-}
-
 size_t csr_scan_temp_bytes(int64_t nb) {
   static thread_local int64_t last_nb = -1;  // the query is per size; remember the last one
   static thread_local size_t last_bytes = 0;
@@ -284,17 +252,7 @@ int launch_csr(const CsrArgs& a, hipStream_t s) {
   e = rocprim::exclusive_scan(a.scan_tmp, bytes, a.cnt, a.off, int32_t(0), (size_t)nb + 1, rocprim::plus<int32_t>(), s);
   if (e != hipSuccess) return (int)e;
   hipLaunchKernelGGL(k_csr_fill, dim3(grid_for(N)), dim3(256), 0, s, a);
-  // bucket-per-wave ranks (KGE_CSR_RANK=1, default) or id-per-thread (0): same output
-  if (env_int_c("KGE_CSR_RANK", 1) == 1)
-    hipLaunchKernelGGL(k_csr_rank_w, dim3((unsigned)((nb + 3) / 4)), dim3(256), 0, s, a, nb);
-  else
-    hipLaunchKernelGGL(k_csr_rank, dim3(grid_for(N)), dim3(256), 0, s, a);
-  return (int)hipGetLastError();
-}
-
-int launch_occ_meta(const MetaArgs& a, hipStream_t s) {
-  if (a.N <= 0) return 0;
-  hipLaunchKernelGGL(k_occ_meta, dim3((unsigned)((a.N + 255) / 256)), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(k_csr_rank_w, dim3((unsigned)((nb + 3) / 4)), dim3(256), 0, s, a, nb);
   return (int)hipGetLastError();
 }
 
@@ -317,20 +275,10 @@ int launch_adam(float* p, const float* g, float* m, float* v, int64_t n, float b
                 float step_size, float bc2s, hipStream_t s) {
   AdamK k;
   k.b1 = b1; k.b2 = b2; k.eps = eps;
-  // KGE_ADAM_VARIANT: 2 (default) non-temporal + 2 float4 groups per thread and
-  // iteration: 5.6 TB/s on the FB15k table against 5.0-5.2 for plain float4 (0);
-  // 1 non-temporal only, 3 two groups only (tools/dbg/adam_rate.py,
-  // profiles/r01/adam_rate_variants.jsonl).  Same per-element math in all.
-  const int var = env_int_c("KGE_ADAM_VARIANT", 2);
+  // non-temporal, two float4 groups per thread and iteration: 5.6 TB/s on the
+  // FB15k table against 5.0-5.2 for plain float4 (profiles/r01/adam_rate_variants.jsonl)
   const dim3 grid(grid_for((n + 3) / 4, 8192));
-  if (var == 1)
-    hipLaunchKernelGGL((k_adam<true, 1>), grid, dim3(256), 0, s, p, g, m, v, n, k, step_size, bc2s);
-  else if (var == 2)
-    hipLaunchKernelGGL((k_adam<true, 2>), grid, dim3(256), 0, s, p, g, m, v, n, k, step_size, bc2s);
-  else if (var == 3)
-    hipLaunchKernelGGL((k_adam<false, 2>), grid, dim3(256), 0, s, p, g, m, v, n, k, step_size, bc2s);
-  else
-    hipLaunchKernelGGL((k_adam<false, 1>), grid, dim3(256), 0, s, p, g, m, v, n, k, step_size, bc2s);
+  hipLaunchKernelGGL((k_adam<true, 2>), grid, dim3(256), 0, s, p, g, m, v, n, k, step_size, bc2s);
   return (int)hipGetLastError();
 }
 

@@ -55,21 +55,14 @@ struct RowArgs {
   float* rel_contrib; // [B, Lr]
   float* row_stats;   // [B, 4]  logσ(s_pos), neg term, d/dmodulus, s_pos
   int n_lds;          // floats reserved for raw scores in LDS (TRAIN: n)
-  int pipe;           // k_row variant: 1 = next row prefetched (3 waves/SIMD), 0 = 4 waves/SIMD
-  int fuse_q;         // 1: k_row builds q (and Σw) itself, no k_build_q launch
-  int fuse_epi;       // 1 (with fuse_q): k_row runs the epilogue in its tail, no k_row_epi launch
+  int fuse_epi;       // 1: k_row runs the epilogue in its tail, no k_row_epi launch
   int32_t* err;
   void (*timer_mid)(hipStream_t);  // stage-timer hook between the row-pass launches (or null)
 };
 
 // k_row's LDS merge buffer: [2][Le] floats, and at least the 256 floats the
 // fused Σw reduction (block_weight_sum) uses as its tree
-// k_row's merge buffer: 2 rows of Le (merge), >= 256 (Σw tree), >= 4 padded
-// half-rows of qp floats (the HP variant's per-wave V im halves)
-__host__ __device__ inline int vb_floats(int Le, int qp) {
-  int v = 2 * Le > 256 ? 2 * Le : 256;
-  return v > 4 * qp ? v : 4 * qp;
-}
+__host__ __device__ inline int vb_floats(int Le) { return 2 * Le > 256 ? 2 * Le : 256; }
 
 struct RelArgs {
   const float* rel;
@@ -84,30 +77,6 @@ struct RelArgs {
   int write_grad;            // store grad_rel (always, unless the optimizer is fused and asks not to)
   AdamT adam;                // fused optimizer step (adam.p == null: none)
   AdamK adamk;
-};
-
-// LDS-tiled entity pass (k_entity_tl): one column tile of q per workgroup
-constexpr int TL_COLS = 32;          // floats of one q row per tile (16 complex or 32 real dims)
-constexpr int TL_STRIDE = TL_COLS + 2;  // LDS row pitch in floats (136 B)
-constexpr int TL_THREADS = 1024;
-constexpr int TL_MAX_ROWS = 1152;    // batch rows that fit: 1152 * 136 B = 153 KiB of the 160 KiB LDS
-
-// Variants of the column-sliced entity pass, selected by KGE_ENT_PF (all
-// bit-identical; measured in DESIGN.md §4).  k_entity_sl<PF, HOIST_ADAM,
-// PACKED, NT, NTP> and the software-pipelined k_entity_pp<EPW, ROWS_EARLY>.
-enum SlicedVariant : int {
-  SL_PF4 = 4,            // 4 q rows in flight, Adam moments loaded after the loop
-  SL_HOIST = 5,          // moments loaded before the loop
-  SL_PACKED = 6,         // + RotatE math on register pairs
-  SL_NT = 7,             // + non-temporal table/moment/gradient stream (default)
-  SL_PF8 = 8,            // 8 q rows in flight
-  SL_NT_MOMENTS = 9,     // SL_NT with the table itself through the caches
-  PP_EARLY2 = 12,        // pipelined, 2 entities per wave, next rows before the Adam tail
-  PP_EARLY4 = 14,        // the same with 4
-  PP1 = 21, PP2 = 22, PP4 = 24, PP8 = 28,  // pipelined, 1/2/4/8 entities per wave
-  SL_LATE_MOMENTS = 30,  // SL_NT with the moments loaded after the loop (7 waves/SIMD)
-  SL_PF3 = 31,           // SL_NT with 3 q rows in flight (6 waves/SIMD)
-  SL_PF2 = 32,           // SL_NT with 2 q rows in flight (7 waves/SIMD)
 };
 
 struct EntArgs {
@@ -129,11 +98,7 @@ struct EntArgs {
   float* reg_partial;   // [E] Σ|x|^3 per row (when reg3 != 0)
   float* grad_ent;
   int write_grad;       // store grad_ent (unless the fused optimizer asks not to)
-  int minw;             // k_entity: min waves/SIMD the register budget targets (3 or 4)
-  int slv;              // column-sliced pass: SlicedVariant
-  int ntiles, ngroups;  // > 0: LDS-tiled pass k_entity_tl (ntiles column tiles x ngroups entity ranges)
   int64_t B;            // batch rows (the q buffer's height)
-  const int2* meta;     // k_entity_tl: per CSR entry (q row or -1, dL/ds bits), from k_occ_meta
   int nsl;              // > 0: column-sliced pass k_entity_sl with nsl slices of slice_w slots (VEC = 4)
   int slice_w;
   AdamT adam;           // fused optimizer step (adam.p == null: none)

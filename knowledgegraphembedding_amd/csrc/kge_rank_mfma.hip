@@ -86,8 +86,8 @@ __device__ __forceinline__ void put(float (*dst)[LDK], const float4 (&r)[F4], in
   }
 }
 
-template <bool GATHER, int MINW>
-__global__ __launch_bounds__(256, MINW) void k_rank_mfma(MfmaArgs a) {
+template <bool GATHER>
+__global__ __launch_bounds__(256, 3) void k_rank_mfma(MfmaArgs a) {
   __shared__ __attribute__((aligned(16))) float As[BM][LDK];
   __shared__ __attribute__((aligned(16))) float Bs[BN][LDK];
   __shared__ int64_t arow[128], brow[128];
@@ -283,18 +283,9 @@ int launch_rank_mfma(const float* q, const float* ent, int64_t nq, int64_t E, in
   const unsigned gy = (unsigned)((nq + BM - 1) / BM);
   // 3 waves/SIMD (158 VGPRs, no spills); 4 fits only with 13 spilled VGPRs
   // and measured 12 % slower
-  static const int minw = [] {
-    const char* e = getenv("KGE_RANK_MFMA_MINW");
-    return e ? atoi(e) : 3;
-  }();
   const dim3 gs((unsigned)((E + BN - 1) / BN), gy);
-  if (minw == 4) {
-    hipLaunchKernelGGL((k_rank_mfma<true, 4>), dim3(1, gy), dim3(256), 0, s, a);
-    hipLaunchKernelGGL((k_rank_mfma<false, 4>), gs, dim3(256), 0, s, a);
-  } else {
-    hipLaunchKernelGGL((k_rank_mfma<true, 3>), dim3(1, gy), dim3(256), 0, s, a);
-    hipLaunchKernelGGL((k_rank_mfma<false, 3>), gs, dim3(256), 0, s, a);
-  }
+  hipLaunchKernelGGL((k_rank_mfma<true>), dim3(1, gy), dim3(256), 0, s, a);
+  hipLaunchKernelGGL((k_rank_mfma<false>), gs, dim3(256), 0, s, a);
   st = (int)hipGetLastError();
   if (st) return st;
   return launch_rank_emit(gt, eq, true_id, nq, ranks, ties, s);

@@ -146,3 +146,28 @@ class BidirectionalOneShotIterator(object):
         while True:
             for data in dataloader:
                 yield data
+
+
+class RankShardSampler(torch.utils.data.Sampler):
+    """Data-parallel training order: each epoch one permutation of the whole
+    train set, drawn from a generator seeded by (seed, epoch) and therefore the
+    same on every rank, of which rank r takes positions r, r + world, ...  The
+    ranks' positives are disjoint within an epoch and together cover it; the
+    epoch advances on every new iteration (BidirectionalOneShotIterator
+    restarts the DataLoader endlessly), so no set_epoch call is needed.  With
+    world = 1 this is a plain reshuffle per epoch."""
+
+    def __init__(self, n: int, rank: int, world: int, seed: int):
+        if world < 1 or not 0 <= rank < world:
+            raise ValueError(f"rank {rank} outside world {world}")
+        self.n, self.rank, self.world, self.seed = int(n), int(rank), int(world), int(seed)
+        self.epoch = 0
+
+    def __len__(self):
+        return (self.n - self.rank + self.world - 1) // self.world
+
+    def __iter__(self):
+        g = torch.Generator().manual_seed(self.seed * 1000003 + self.epoch)
+        self.epoch += 1
+        perm = torch.randperm(self.n, generator=g)
+        return iter(perm[self.rank::self.world].tolist())

@@ -25,7 +25,7 @@ import numpy as np
 import torch
 from torch.utils.data import DataLoader
 
-from .dataloader import BidirectionalOneShotIterator, TrainDataset
+from .dataloader import BidirectionalOneShotIterator, RankShardSampler, TrainDataset
 from .model import KGEModel
 from .optim import KGEAdam
 
@@ -129,6 +129,26 @@ def read_dict(file_path):
             eid, name = line.strip().split('\t')
             out[name] = int(eid)
     return out
+
+
+def make_train_iterator(args, train_triples, nentity, nrelation, rank=0, world=1):
+    """run.py:246-259's two DataLoaders and BidirectionalOneShotIterator.  One
+    process: exactly the reference's (shuffle=True on torch's global
+    generator).  Under data parallelism each rank gets a disjoint shard of
+    every epoch's permutation (RankShardSampler, same seed on all ranks) and
+    its own generator, so its workers' numpy streams — the negatives — differ
+    from the other ranks' too."""
+    def loader(mode):
+        ds = TrainDataset(train_triples, nentity, nrelation, args.negative_sample_size, mode)
+        kw = dict(batch_size=args.batch_size, num_workers=max(1, args.cpu_num // 2),
+                  collate_fn=TrainDataset.collate_fn)
+        if world <= 1:
+            return DataLoader(ds, shuffle=True, **kw)
+        seed = int(torch.initial_seed()) % (1 << 31)
+        return DataLoader(ds, sampler=RankShardSampler(len(ds), rank, world, seed + (mode == 'tail-batch')),
+                          generator=torch.Generator().manual_seed(seed + 7919 * (rank + 1)), **kw)
+
+    return BidirectionalOneShotIterator(loader('head-batch'), loader('tail-batch'))
 
 
 def set_logger(args, rank=0):
@@ -247,15 +267,8 @@ def main(args):
                                              args.batch_size, kge_model.entity_embedding.device,
                                              seed=torch.initial_seed() + rank)
     elif args.do_train:
-        train_dataloader_head = DataLoader(
-            TrainDataset(train_triples, nentity, nrelation, args.negative_sample_size, 'head-batch'),
-            batch_size=args.batch_size, shuffle=True, num_workers=max(1, args.cpu_num // 2),
-            collate_fn=TrainDataset.collate_fn)
-        train_dataloader_tail = DataLoader(
-            TrainDataset(train_triples, nentity, nrelation, args.negative_sample_size, 'tail-batch'),
-            batch_size=args.batch_size, shuffle=True, num_workers=max(1, args.cpu_num // 2),
-            collate_fn=TrainDataset.collate_fn)
-        train_iterator = BidirectionalOneShotIterator(train_dataloader_head, train_dataloader_tail)
+        world = 1 if args.dp_group is None else torch.distributed.get_world_size(args.dp_group)
+        train_iterator = make_train_iterator(args, train_triples, nentity, nrelation, rank, world)
     if args.do_train:
         current_learning_rate = args.learning_rate
         optimizer = KGEAdam(trainable(), lr=current_learning_rate)

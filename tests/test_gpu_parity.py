@@ -466,28 +466,21 @@ def test_config2_full_size_properties():
                                       ("pRotatE", 200, 24), ("DistMult", 200, 24), ("RotatE", 104, 1100),
                                       ("DistMult", 52, 700)])
 def test_entity_pass_column_slices_bitwise(name, d, B, monkeypatch):
-    """The LDS-tiled entity pass (k_entity_tl, KGE_ENT_TILE=1), the column-sliced
-    pass (k_entity_sl, nsl = 1, 2, 4, 8 slices; the default), its software-pipelined form
-    (k_entity_pp, KGE_ENT_PF = 12..28: 1, 2, 4 or 8 entities per wave), its 30-32 register
-    budgets and the row-per-wave pass
-    (KGE_ENT_TILE=0 KGE_ENT_SLICES=0) apply the same per-element arithmetic in
-    the same occurrence order: identical gradients and fused Adam updates, bit
-    for bit (the regulariser's partial sums only regroup).  d = 200 / 104 / 52
-    leave the last 16-column tile partial; B = 1100 fills most of the LDS."""
+    """The column-sliced entity pass (k_entity_sl with nsl = 1, 2, 4, 8
+    slices — the count is picked per shape) and the row-per-wave pass
+    (k_entity, the path for rows that are not float4-aligned; KGE_ENT_SLICES=0
+    forces it here) apply the same per-element arithmetic in the same
+    occurrence order: identical gradients and fused Adam updates, bit for bit
+    (the regulariser's partial sums only regroup)."""
     E, R, n = 300, 7, 40   # d = 200: 50 slots per (half) row: 1..8 slices all fit
     args = Namespace(negative_adversarial_sampling=True, adversarial_temperature=1.0, uni_weight=False,
                      regularization=1e-4 if name in ("ComplEx", "DistMult") else 0.0)
     pos, neg, w = synth.kge_batch(88, B, n, E, R)
     P, N, W = torch.from_numpy(pos).to(DEV), torch.from_numpy(neg).to(DEV), torch.from_numpy(w).to(DEV)
     out = {}
-    # "pf<k>": KGE_ENT_PF=k on 4 slices — k_entity_sl with other register budgets
-    # (30-32) and the software-pipelined k_entity_pp (12-28)
-    pipelined = ("pf12", "pf14", "pf21", "pf22", "pf24", "pf28", "pf30", "pf31", "pf32")
-    variants = (("0", "1", "2", "4", "8", "tile") if d == 200 else ("0", "tile")) + pipelined
+    variants = ("0", "1", "2", "4", "8") if d == 200 else ("0", "-1")
     for nsl in variants:
-        monkeypatch.setenv("KGE_ENT_TILE", "1" if nsl == "tile" else "0")
-        monkeypatch.setenv("KGE_ENT_SLICES", "0" if nsl == "tile" else ("4" if nsl.startswith("pf") else nsl))
-        monkeypatch.setenv("KGE_ENT_PF", nsl[2:] if nsl.startswith("pf") else "7")
+        monkeypatch.setenv("KGE_ENT_SLICES", nsl)
         m, *_ = build_model(name, E, R, d, 12.0, 5)
         opt = KGEAdam([p for p in m.parameters() if p.requires_grad], lr=1e-3)
         res = []
@@ -505,42 +498,34 @@ def test_entity_pass_column_slices_bitwise(name, d, B, monkeypatch):
 
 @pytest.mark.parametrize("name,E,d,B,n", [(nm, 400, 120, 24, 40) for nm in NAMES] +
                          [("RotatE", 300, 64, 8, 32), ("RotatE", 2000, 100, 64, 32), ("DistMult", 500, 16, 300, 8)])
-def test_fused_q_build_bitwise(name, E, d, B, n, monkeypatch):
-    """k_row building q and Σw in its own prologue (KGE_FUSE_Q=1), and also
-    running the epilogue in its tail (KGE_FUSE_EPI=1), give the separate
-    launches' losses and gradients bit for bit (same per-element arithmetic,
-    same fixed-order Σw reduction, same epilogue function).  Many blocks per
-    launch (B = 64, 300) exercise the fused tail's c_i, which must not read the
-    Σw that block 0 publishes in the same launch; d = 16 with B = 300 needs the
-    Σw tree's 256 floats of LDS beyond the 2·Le merge buffer.  The row-pass
-    pipelines (KGE_ROW_PIPE = 1, 2) must give the same bits as well."""
+def test_fused_epilogue_bitwise(name, E, d, B, n):
+    """k_row with the epilogue in its tail (the single-call step) and the
+    separate k_row_epi launch (the phased step the data-parallel overlap uses)
+    give the same losses and gradients bit for bit: same per-element
+    arithmetic, same fixed-order Σw reduction, same epilogue function.  Many
+    blocks per launch (B = 64, 300) exercise the fused tail's c_i, which must
+    not read the Σw that block 0 publishes in the same launch; d = 16 with
+    B = 300 needs the Σw tree's 256 floats of LDS beyond the 2·Le merge buffer."""
     R = 9
     pos, neg, w = synth.kge_batch(91, B, n, E, R)
     P, N, W = torch.from_numpy(pos).to(DEV), torch.from_numpy(neg).to(DEV), torch.from_numpy(w).to(DEV)
     res = {}
-    # + the row-pass pipelines: "hp" = KGE_ROW_PIPE=2 (RotatE: V's im half in
-    # LDS, next row's re half in flight; fused), "hp0" the same unfused, "pipe"
-    # = KGE_ROW_PIPE=1 (whole next row in registers)
-    variants = {"0": ("0", "0", "0"), "1": ("1", "0", "0"), "epi": ("1", "1", "0"), "hp": ("1", "1", "2"),
-                "hp0": ("0", "0", "2"), "pipe": ("0", "0", "1")}
-    for fq, (fuse_q, fuse_epi, pipe) in variants.items():
-        monkeypatch.setenv("KGE_FUSE_Q", fuse_q)
-        monkeypatch.setenv("KGE_FUSE_EPI", fuse_epi)
-        monkeypatch.setenv("KGE_ROW_PIPE", pipe)
+    for phased in (False, True):
         out = []
+        chunks = [(0, E)] if phased else None
         for adv, uni in ((True, False), (False, True)):
             m, *_ = build_model(name, E, R, d, 12.0, 7)
             args = Namespace(negative_adversarial_sampling=adv, adversarial_temperature=0.7, uni_weight=uni,
                              regularization=0.0)
             for mode in ("tail-batch", "head-batch"):
-                losses = m.compute_train_grads(P, N, W, mode, args)
+                losses = m.compute_train_grads(P, N, W, mode, args, entity_chunks=chunks)
                 out.append([t.detach().cpu().clone() for t in (losses, m.entity_embedding.grad,
                                                                m.relation_embedding.grad)])
             # Σw supplied by the caller (the data-parallel path)
-            losses = m.compute_train_grads(P, N, W, "tail-batch", args, weight_sum=W.sum().reshape(1))
+            losses = m.compute_train_grads(P, N, W, "tail-batch", args, weight_sum=W.sum().reshape(1),
+                                           entity_chunks=chunks)
             out.append([losses.detach().cpu().clone(), m.entity_embedding.grad.cpu().clone()])
-        res[fq] = out
-    for variant in list(variants)[1:]:
-        for a, b in zip(res["0"], res[variant]):
-            for x, y in zip(a, b):
-                assert torch.equal(x, y), variant
+        res[phased] = out
+    for a, b in zip(res[False], res[True]):
+        for x, y in zip(a, b):
+            assert torch.equal(x, y)

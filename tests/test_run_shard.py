@@ -1,0 +1,73 @@
+"""run.py's training iterator under data parallelism (every rank
+used to draw the same positives and negatives).  make_train_iterator with
+world = 2 gives each rank a disjoint half of every epoch's positives, different
+negatives, and together the whole train set; world = 1 keeps the reference's
+DataLoader(shuffle=True)."""
+from argparse import Namespace
+
+import numpy as np
+import torch
+
+from knowledgegraphembedding_amd import synth
+from knowledgegraphembedding_amd.dataloader import RankShardSampler
+from knowledgegraphembedding_amd.run import make_train_iterator
+
+E, R, NTR = 50, 4, 96
+
+
+def _triples():
+    h = synth.randint(5, (NTR,), E)
+    r = synth.randint(6, (NTR,), R)
+    t = synth.randint(7, (NTR,), E)
+    return sorted(set(map(tuple, np.stack([h, r, t], 1).tolist())))
+
+
+def _epoch(it, nbatches):
+    pos, neg = [], []
+    for _ in range(nbatches):
+        p, n, w, mode = next(it)
+        pos.append(p)
+        neg.append(n)
+    return pos, neg
+
+
+def test_rank_shard_sampler_partitions_each_epoch():
+    s0, s1 = RankShardSampler(11, 0, 2, 3), RankShardSampler(11, 1, 2, 3)
+    for _ in range(3):
+        a, b = list(s0), list(s1)
+        assert len(a) == len(s0) == 6 and len(b) == len(s1) == 5
+        assert sorted(a + b) == list(range(11))
+    e0, e1 = list(RankShardSampler(11, 0, 1, 3)), list(RankShardSampler(11, 0, 1, 3))
+    assert e0 == e1  # same seed and epoch → same order on every rank
+
+
+def test_ranks_draw_disjoint_positives_and_different_negatives():
+    triples = _triples()
+    args = Namespace(negative_sample_size=8, batch_size=8, cpu_num=2)
+    torch.manual_seed(11)
+    it0 = make_train_iterator(args, triples, E, R, rank=0, world=2)
+    torch.manual_seed(11)
+    it1 = make_train_iterator(args, triples, E, R, rank=1, world=2)
+    half = len(triples) // 2
+    nb = 2 * ((half + 7) // 8)  # tail + head batches covering one epoch of each loader
+    p0, n0 = _epoch(it0, nb)
+    p1, n1 = _epoch(it1, nb)
+    # BidirectionalOneShotIterator alternates tail (odd) / head (even) loaders:
+    # every other batch belongs to one loader's epoch
+    def loader_rows(p, first):  # batches 0, 2, 4, ... are the tail loader's
+        return {tuple(x) for k in range(first, nb, 2) for x in p[k].tolist()}
+
+    for first in (0, 1):
+        a, b = loader_rows(p0, first), loader_rows(p1, first)
+        assert not (a & b)                     # disjoint within the epoch
+        assert a | b == set(triples)           # and together the whole train set
+    assert not torch.equal(n0[0], n1[0])
+
+
+def test_single_process_keeps_reference_loader():
+    triples = _triples()
+    args = Namespace(negative_sample_size=4, batch_size=4, cpu_num=2)
+    it = make_train_iterator(args, triples, E, R)
+    assert isinstance(it.iterator_head, type(it.iterator_tail))
+    p, n, w, mode = next(it)
+    assert mode == "tail-batch" and p.shape == (4, 3) and n.shape == (4, 4)

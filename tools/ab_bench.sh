@@ -1,6 +1,6 @@
 #!/bin/bash
 # A/B: run bench.py once per env-variant string given as arguments, e.g.
-#   tools/ab_bench.sh "KGE_ENT_TILE=0" "KGE_ENT_TILE=1"
+#   tools/ab_bench.sh "KGE_ENT_SLICES=4" "KGE_ENT_SLICES=8"
 # Each line of gpurun_out/ab.jsonl = {"env": ..., bench JSON}.  Stops at the first failure.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"

@@ -54,7 +54,7 @@ def main():
     main_bytes = (sum(v["hbm_bytes_per_launch"] * v["launches"] for v in sel.values()) / tot_l) if tot_l else None
     out = {"kernel": a.kernel, "hbm_bytes_per_launch": main_bytes,
            "method": "(2*FETCH_SIZE + WRITE_SIZE) KiB * 1024, separate --pmc passes (MI355X_MICROARCH.md HBM)",
-           "kernels": summary}
+           "kernels": sel}
     s = json.dumps(out, indent=1)
     if a.out:
         with open(a.out, "w") as fh:
