@@ -152,6 +152,24 @@ def _cpu_model() -> str:
     return "unknown"
 
 
+def host_cores() -> int:
+    """CPUs this process may actually use: the affinity mask, capped by the
+    cgroup CPU quota and OMP_NUM_THREADS when set (a GPU box shows all of the
+    machine's cores in the mask but grants a share of them)."""
+    n = len(os.sched_getaffinity(0))
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota, period = f.read().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, -(-int(quota) // int(period))))
+    except (OSError, ValueError):
+        pass
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    if omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
+    return n
+
+
 def cpu_baseline(model_cpu_state, budget_s: float = 12.0, b: int = 32):
     """The oracle (reference op chain on CPU fp32, + torch.optim.Adam) on a
     bounded sample of the same workload: b positives x 256 negatives, on every
@@ -162,7 +180,7 @@ def cpu_baseline(model_cpu_state, budget_s: float = 12.0, b: int = 32):
     the line carries that ratio next to the sample."""
     from oracle import kge_oracle as O
     ent, rel, erange = model_cpu_state
-    cores = len(os.sched_getaffinity(0))
+    cores = host_cores()
     torch.set_num_threads(cores)
     g = torch.Generator().manual_seed(7)
     pos = torch.stack([torch.randint(0, E, (b,), generator=g), torch.randint(0, R, (b,), generator=g),

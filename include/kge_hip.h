@@ -276,12 +276,31 @@ int kge_adam_step(float *param, const float *grad, float *exp_avg, float *exp_av
  *   ranks_out [nq] int64: 1 + #{unfiltered e != true : score_e > score_true}.
  *   ties_out  [nq] int32 (nullable): #{unfiltered e != true : score_e == score_true}
  *   (the reference's argsort is not stable; a tie may land either side).
+ * "score" is the reference's own fp32 score: a fast fp32 pass counts every
+ * candidate whose score clears the true one's by more than a rounding bound
+ * and lists the rest, which are re-scored in the reference's operation order
+ * (the ATen elementwise ops and its sum(dim=2) / norm(p=1) reduction order) —
+ * bit-exact to the reference for TransE, DistMult and ComplEx; RotatE and
+ * pRotatE use correctly rounded cos/sin where the reference uses its CPU
+ * vector library's (last-bit differences on a few percent of arguments).
  */
 size_t kge_rank_workspace_bytes(const kge_model_desc *m, int64_t nq);
 int kge_rank_filtered(const kge_model_desc *m, int32_t mode, const int64_t *queries, int64_t nq,
                       const int64_t *filt_off, const int64_t *filt_ids, int64_t *ranks_out,
                       int32_t *ties_out, void *workspace, size_t workspace_bytes, int32_t *err_flag,
                       void *stream);
+/*
+ * The same with the fast pass chosen (path: 0 auto, 1 MFMA tile — DistMult /
+ * ComplEx with float4-aligned rows, 2 register tile — reduction length % 4 ==
+ * 0, 3 wave scan; KGE_ERR_ARG if the rows do not suit the requested path) and
+ * listed_out [nq] int32 (nullable): near-ties re-scored per query (above the
+ * 1024-per-query list capacity the query is rescanned exactly).  Every path
+ * returns the same ranks and ties.
+ */
+int kge_rank_filtered_ex(const kge_model_desc *m, int32_t mode, const int64_t *queries, int64_t nq,
+                         const int64_t *filt_off, const int64_t *filt_ids, int64_t *ranks_out,
+                         int32_t *ties_out, int32_t *listed_out, int32_t path, void *workspace,
+                         size_t workspace_bytes, int32_t *err_flag, void *stream);
 
 /*
  * Live stage timing for benchmarks (no reference counterpart): when enabled,

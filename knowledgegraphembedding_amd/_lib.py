@@ -104,6 +104,7 @@ SIGNATURES = {
     "kge_adam_step": (C.c_int, [_P, _P, _P, _P, _I64, _F, _F, _F, _F, _F, _P]),
     "kge_rank_workspace_bytes": (_SZ, [_DESC, _I64]),
     "kge_rank_filtered": (C.c_int, [_DESC, _I32, _P, _I64, _P, _P, _P, _P, _P, _SZ, _P, _P]),
+    "kge_rank_filtered_ex": (C.c_int, [_DESC, _I32, _P, _I64, _P, _P, _P, _P, _P, _I32, _P, _SZ, _P, _P]),
     "kge_stage_timer": (C.c_int, [_I32, _P, _I32]),
     "kge_sample_negatives": (C.c_int, [_P, _I64, _P, _I64, _I64, _I64, _P, _P, _P, _P, C.c_uint64, _I64, _P, _P, _P,
                                        _P, _P]),

@@ -61,26 +61,25 @@ int check_model(const kge_model_desc* m, Geom* g) {
   return KGE_OK;
 }
 
-// DistMult / ComplEx scores are <q, e>: ranked on the matrix cores when rows
-// are float4-aligned (KGE_RANK_MFMA=0 forces the VALU scan, for A/B runs).
-bool use_mfma_rank(const kge_model_desc* m) {
-  const char* ev = getenv("KGE_RANK_MFMA");  // read per call: ranking launches are few and large
-  const int on = ev ? atoi(ev) : 1;
-  return on && (m->model == KGE_DISTMULT || m->model == KGE_COMPLEX) && (m->entity_dim % 4 == 0) &&
-         aligned16(m->entity_embedding);
-}
-
-// Register-tiled ranking (k_rank_tile) for the models without an MFMA form,
-// and for the bilinear ones when KGE_RANK_MFMA=0.  Needs the reduction length
-// divisible by 4 (float4 staging); KGE_RANK_TILE=0 selects the per-pair
-// wave-reduction scan instead.
-bool use_tile_rank(const kge_model_desc* m) {
-  const char* ev = getenv("KGE_RANK_TILE");
-  const int on = ev ? atoi(ev) : 1;
+// Fast counting pass of the filtered ranking (path 0 = auto): the fp32 MFMA
+// tile for DistMult / ComplEx with float4-aligned rows, the register tile for
+// the others when the reduction length is a multiple of 4, the wave scan
+// otherwise.  Every path ends in the same reference-order refinement, so all
+// give the same ranks.
+enum RankPath : int { RP_AUTO = 0, RP_MFMA = 1, RP_TILE = 2, RP_SCAN = 3 };
+int rank_path(const kge_model_desc* m, int requested) {
+  const bool bil = (m->model == KGE_DISTMULT || m->model == KGE_COMPLEX);
   const bool cplx = (m->model == KGE_ROTATE || m->model == KGE_COMPLEX);
   const int K = cplx ? m->entity_dim / 2 : m->entity_dim;
-  return on && !use_mfma_rank(m) && (K % 4 == 0) && aligned16(m->entity_embedding);
+  const bool al = aligned16(m->entity_embedding);
+  const bool mfma_ok = bil && (m->entity_dim % 4 == 0) && al;
+  const bool tile_ok = (K % 4 == 0) && al;
+  if (requested == RP_MFMA) return mfma_ok ? RP_MFMA : -1;
+  if (requested == RP_TILE) return tile_ok ? RP_TILE : -1;
+  if (requested == RP_SCAN) return RP_SCAN;
+  return mfma_ok ? RP_MFMA : (tile_ok ? RP_TILE : RP_SCAN);
 }
+constexpr int RANK_CAP = 1024;  // listed near-ties per query before the exact rescan takes over
 
 Consts consts_of(const kge_model_desc* m) {
   Consts c;
@@ -655,69 +654,144 @@ int kge_adam_step(float* param, const float* grad, float* exp_avg, float* exp_av
                                    bias_correction2_sqrt, as_stream(stream)));
 }
 
+}  // extern "C"
+
+namespace kge {
+namespace {
+struct RankWs {
+  float *q, *qref, *s_true, *sref_true, *delta, *stats;
+  int64_t* true_id;
+  int32_t *gt, *eq, *gtx, *eqx, *ucnt, *ulist;
+  uint32_t* bits;
+};
+RankWs carve_rank(void* ws, const kge_model_desc* m, int64_t nq, size_t* bytes) {
+  Carver c(ws);
+  RankWs w;
+  w.q = c.take<float>(nq * (int64_t)m->entity_dim);
+  w.qref = c.take<float>(nq * (int64_t)m->entity_dim);
+  w.s_true = c.take<float>(nq);
+  w.sref_true = c.take<float>(nq);
+  w.delta = c.take<float>(nq);
+  w.stats = c.take<float>(4);
+  w.true_id = c.take<int64_t>(nq);
+  w.gt = c.take<int32_t>(5 * nq);  // gt, eq, gtx, eqx, ucnt: one memset
+  w.eq = w.gt ? w.gt + nq : nullptr;
+  w.gtx = w.gt ? w.gt + 2 * nq : nullptr;
+  w.eqx = w.gt ? w.gt + 3 * nq : nullptr;
+  w.ucnt = w.gt ? w.gt + 4 * nq : nullptr;
+  w.ulist = c.take<int32_t>(nq * (int64_t)RANK_CAP);
+  w.bits = c.take<uint32_t>(nq * ((m->nentity + 31) / 32));
+  *bytes = c.off + 256;
+  return w;
+}
+}  // namespace
+}  // namespace kge
+
+extern "C" {
+
 size_t kge_rank_workspace_bytes(const kge_model_desc* m, int64_t nq) {
-  Carver c(nullptr);
-  c.take<float>(nq * (int64_t)m->entity_dim);
-  c.take<float>(nq);
-  c.take<int64_t>(nq);
-  c.take<int32_t>(nq);
-  c.take<int32_t>(nq);
-  if (use_mfma_rank(m) || use_tile_rank(m)) c.take<uint32_t>(nq * ((m->nentity + 31) / 32));  // filtered-candidate bitmap
-  return c.off + 256;
+  size_t b = 0;
+  carve_rank(nullptr, m, nq, &b);
+  return b;
 }
 
-int kge_rank_filtered(const kge_model_desc* m, int32_t mode, const int64_t* queries, int64_t nq,
-                      const int64_t* filt_off, const int64_t* filt_ids, int64_t* ranks_out, int32_t* ties_out,
-                      void* workspace, size_t workspace_bytes, int32_t* err_flag, void* stream) {
+int kge_rank_filtered_ex(const kge_model_desc* m, int32_t mode, const int64_t* queries, int64_t nq,
+                         const int64_t* filt_off, const int64_t* filt_ids, int64_t* ranks_out, int32_t* ties_out,
+                         int32_t* listed_out, int32_t path, void* workspace, size_t workspace_bytes,
+                         int32_t* err_flag, void* stream) {
   Geom geo;
   int st = check_model(m, &geo);
   if (st) return st;
   if (mode != KGE_HEAD_BATCH && mode != KGE_TAIL_BATCH) return KGE_ERR_MODE;
   if (!queries || !filt_off || !ranks_out || !err_flag || nq < 0) return KGE_ERR_ARG;
+  if (path < RP_AUTO || path > RP_SCAN) return KGE_ERR_ARG;
   if (nq == 0) return KGE_OK;
-  if (workspace_bytes < kge_rank_workspace_bytes(m, nq) || !workspace) return KGE_ERR_WORKSPACE;
-  Carver c(workspace);
+  if (nq > 65535) return KGE_ERR_DIM;  // the bitmap launch puts queries on grid.y
+  const int rp = rank_path(m, path);
+  if (rp < 0) return KGE_ERR_ARG;  // the requested fast pass cannot take these rows
+  size_t need = 0;
+  RankWs w = carve_rank(workspace, m, nq, &need);
+  if (!workspace || workspace_bytes < need) return KGE_ERR_WORKSPACE;
+  hipStream_t s = as_stream(stream);
+  hipError_t e = hipMemsetAsync(w.gt, 0, sizeof(int32_t) * 5 * nq, s);
+  if (e != hipSuccess) return hip_status(e);
+  const ModelOps& ops = ops_for(m->model);
+  const bool cplx = (m->model == KGE_ROTATE || m->model == KGE_COMPLEX);
+  const int K = cplx ? m->entity_dim / 2 : m->entity_dim;
+  RankWin win;
+  win.delta = w.delta; win.ucnt = w.ucnt; win.ulist = w.ulist; win.cap = RANK_CAP;
+
+  // 1. q, true ids (and, for the wave scan, s_true)
   RankArgs a;
+  memset(&a, 0, sizeof(a));
   a.ent = m->entity_embedding; a.rel = m->relation_embedding; a.modulus = m->modulus;
   a.queries = queries; a.nq = nq; a.E = m->nentity; a.R = m->nrelation;
   a.Le = m->entity_dim; a.Lr = m->relation_dim; a.eg = geo.eg; a.c = consts_of(m);
   a.filt_off = filt_off; a.filt_ids = filt_ids;
   a.cpw = 64;
-  a.q = c.take<float>(nq * (int64_t)m->entity_dim);
-  a.s_true = c.take<float>(nq);
-  a.true_id = c.take<int64_t>(nq);
-  a.gt = c.take<int32_t>(nq);
-  a.eq = c.take<int32_t>(nq);
-  a.ranks = ranks_out; a.ties = ties_out; a.err = err_flag;
-  hipStream_t s = as_stream(stream);
-  hipError_t e = hipMemsetAsync(a.gt, 0, sizeof(int32_t) * nq, s);
-  if (e != hipSuccess) return hip_status(e);
-  e = hipMemsetAsync(a.eq, 0, sizeof(int32_t) * nq, s);
-  if (e != hipSuccess) return hip_status(e);
-  const bool mfma = use_mfma_rank(m) && nq <= 65535;
-  const bool tile = !mfma && use_tile_rank(m) && nq <= 65535;
-  a.prep_only = (mfma || tile) ? 1 : 0;
-  st = launch_status(ops_for(m->model).rank(mode, geo.vec, geo.ns, a, s));
-  if (st || !(mfma || tile)) return st;
-  uint32_t* bits = c.take<uint32_t>(nq * ((m->nentity + 31) / 32));
-  if (mfma)  // bilinear models: S = Q · Eᵀ on the matrix cores (kge_rank_mfma.hip)
-    return launch_status(launch_rank_mfma(a.q, m->entity_embedding, nq, m->nentity, m->entity_dim, a.true_id,
-                                          a.s_true, filt_off, filt_ids, bits, a.gt, a.eq, ranks_out, ties_out,
-                                          err_flag, s));
-  st = launch_status(launch_filter_bits(filt_off, filt_ids, a.true_id, nq, m->nentity, bits, err_flag, s));
+  a.q = w.q; a.s_true = w.s_true; a.true_id = w.true_id; a.gt = w.gt;
+  a.fbits = w.bits; a.W = (m->nentity + 31) / 32; a.win = win; a.err = err_flag;
+  a.prep_only = 1;
+  st = launch_status(ops.rank(mode, geo.vec, geo.ns, a, s));
   if (st) return st;
+  // 2. excluded candidates (filtered ids + the true id) as a bitmap
+  st = launch_status(launch_filter_bits(filt_off, filt_ids, w.true_id, nq, m->nentity, w.bits, err_flag, s));
+  if (st) return st;
+  if (m->model == KGE_DISTMULT || m->model == KGE_COMPLEX || m->model == KGE_PROTATE) {
+    st = launch_status(launch_table_stats(m->entity_embedding, m->nentity, m->entity_dim, w.stats, s));
+    if (st) return st;
+  }
+  // 3. the fast pass's own s_true (same instruction sequence as its candidates)
   TileArgs ta;
-  ta.q = a.q; ta.ent = m->entity_embedding; ta.modulus = m->modulus;
-  ta.nq = nq; ta.E = m->nentity; ta.Le = m->entity_dim;
-  ta.K = (m->model == KGE_ROTATE || m->model == KGE_COMPLEX) ? m->entity_dim / 2 : m->entity_dim;
-  ta.c = a.c; ta.true_id = a.true_id; ta.s_true = a.s_true;
-  ta.fbits = bits; ta.W = (m->nentity + 31) / 32; ta.gt = a.gt; ta.eq = a.eq;
-  const ModelOps& ops = ops_for(m->model);
-  st = launch_status(ops.rank_tile(mode, 1, ta, s));
+  ta.q = w.q; ta.ent = m->entity_embedding; ta.modulus = m->modulus;
+  ta.nq = nq; ta.E = m->nentity; ta.Le = m->entity_dim; ta.K = K;
+  ta.c = a.c; ta.true_id = w.true_id; ta.s_true = w.s_true;
+  ta.fbits = w.bits; ta.W = a.W; ta.gt = w.gt; ta.win = win;
+  if (rp == RP_MFMA)
+    st = launch_status(launch_rank_mfma(1, w.q, m->entity_embedding, nq, m->nentity, m->entity_dim, w.true_id,
+                                        w.s_true, w.bits, w.gt, win, s));
+  else if (rp == RP_TILE)
+    st = launch_status(ops.rank_tile(mode, 1, ta, s));
   if (st) return st;
-  st = launch_status(ops.rank_tile(mode, 0, ta, s));
+  // 4. near-tie windows and the reference-order q
+  RefArgs ra;
+  ra.ent = m->entity_embedding; ra.rel = m->relation_embedding; ra.modulus = m->modulus;
+  ra.queries = queries; ra.nq = nq; ra.E = m->nentity; ra.R = m->nrelation;
+  ra.Le = m->entity_dim; ra.Lr = m->relation_dim; ra.K = K; ra.c = a.c;
+  ra.q = w.q; ra.qref = w.qref; ra.true_id = w.true_id; ra.s_true = w.s_true; ra.sref_true = w.sref_true;
+  ra.delta = w.delta; ra.stats = w.stats;
+  ra.exact_fast = (m->model == KGE_TRANSE && rp == RP_TILE) ? 1 : 0;
+  ra.ucnt = w.ucnt; ra.ulist = w.ulist; ra.cap = RANK_CAP;
+  ra.fbits = w.bits; ra.W = a.W; ra.gt = w.gt; ra.eq = w.eq; ra.gtx = w.gtx; ra.eqx = w.eqx; ra.err = err_flag;
+  st = launch_status(ops.rank_ref(mode, 0, ra, s));
   if (st) return st;
-  return launch_status(launch_rank_emit(a.gt, a.eq, a.true_id, nq, ranks_out, ties_out, s));
+  // 5. fast counting pass: clear cases counted, near-ties listed
+  if (rp == RP_MFMA) {
+    st = launch_status(launch_rank_mfma(0, w.q, m->entity_embedding, nq, m->nentity, m->entity_dim, w.true_id,
+                                        w.s_true, w.bits, w.gt, win, s));
+  } else if (rp == RP_TILE) {
+    st = launch_status(ops.rank_tile(mode, 0, ta, s));
+  } else {
+    a.prep_only = 0;
+    st = launch_status(ops.rank(mode, geo.vec, geo.ns, a, s));
+  }
+  if (st) return st;
+  // 6. refinement in the reference's operation order; exact rescan on overflow
+  st = launch_status(ops.rank_ref(mode, 1, ra, s));
+  if (st) return st;
+  st = launch_status(ops.rank_ref(mode, 2, ra, s));
+  if (st) return st;
+  EmitArgs ea;
+  ea.gt = w.gt; ea.eq = w.eq; ea.gtx = w.gtx; ea.eqx = w.eqx; ea.ucnt = w.ucnt; ea.true_id = w.true_id;
+  ea.nq = nq; ea.cap = RANK_CAP; ea.ranks = ranks_out; ea.ties = ties_out; ea.listed = listed_out;
+  return launch_status(launch_rank_emit(ea, s));
+}
+
+int kge_rank_filtered(const kge_model_desc* m, int32_t mode, const int64_t* queries, int64_t nq,
+                      const int64_t* filt_off, const int64_t* filt_ids, int64_t* ranks_out, int32_t* ties_out,
+                      void* workspace, size_t workspace_bytes, int32_t* err_flag, void* stream) {
+  return kge_rank_filtered_ex(m, mode, queries, nq, filt_off, filt_ids, ranks_out, ties_out, nullptr, RP_AUTO,
+                              workspace, workspace_bytes, err_flag, stream);
 }
 
 int kge_stage_timer(int32_t command, float* stage_ms_out, int32_t n_out) {

@@ -37,13 +37,22 @@ struct FinArgs {
   AdamK adamk;
 };
 
-int launch_rank_mfma(const float* q, const float* ent, int64_t nq, int64_t E, int K, const int64_t* true_id,
-                     float* s_true, const int64_t* filt_off, const int64_t* filt_ids, uint32_t* bits, int32_t* gt,
-                     int32_t* eq, int64_t* ranks, int32_t* ties, int32_t* err, hipStream_t s);
+int launch_rank_mfma(int gather, const float* q, const float* ent, int64_t nq, int64_t E, int K,
+                     const int64_t* true_id, float* s_true, const uint32_t* bits, int32_t* gt, const RankWin& win,
+                     hipStream_t s);
+int launch_table_stats(const float* ent, int64_t E, int Le, float* stats, hipStream_t s);
 int launch_filter_bits(const int64_t* filt_off, const int64_t* filt_ids, const int64_t* true_id, int64_t nq,
                        int64_t E, uint32_t* bits, int32_t* err, hipStream_t s);
-int launch_rank_emit(const int32_t* gt, const int32_t* eq, const int64_t* true_id, int64_t nq, int64_t* ranks,
-                     int32_t* ties, hipStream_t s);
+struct EmitArgs {
+  const int32_t *gt, *eq, *gtx, *eqx, *ucnt;
+  const int64_t* true_id;
+  int64_t nq;
+  int cap;
+  int64_t* ranks;
+  int32_t* ties;    // may be null
+  int32_t* listed;  // may be null: near-ties listed per query (diagnostics)
+};
+int launch_rank_emit(const EmitArgs& a, hipStream_t s);
 size_t csr_scan_temp_bytes(int64_t nb);
 int launch_csr(const CsrArgs& a, hipStream_t s);
 int launch_rel_rows(const RelArgs& a, hipStream_t s);

@@ -107,6 +107,27 @@ struct EntArgs {
   int64_t rel_blocks;
 };
 
+// Near-tie window of the fast ranking passes (all three): a candidate whose
+// fast fp32 score lies within delta[q] of the query's fast true score is not
+// counted but listed for the reference-order refinement (kge_rank_ref.h).
+struct RankWin {
+  const float* delta;  // [nq]
+  int32_t* ucnt;       // [nq]  listed candidates (may exceed cap: overflow)
+  int32_t* ulist;      // [nq, cap]
+  int cap;
+};
+
+__device__ __forceinline__ void win_count(const RankWin& w, int64_t q, int64_t e, float s, float st, float dlt,
+                                          int& g) {
+  const float diff = s - st;
+  if (diff > dlt) {
+    ++g;
+  } else if (diff >= -dlt) {
+    const int idx = atomicAdd(&w.ucnt[q], 1);
+    if (idx < w.cap) w.ulist[q * (int64_t)w.cap + idx] = (int32_t)e;
+  }
+}
+
 struct RankArgs {
   const float* ent;
   const float* rel;
@@ -123,11 +144,40 @@ struct RankArgs {
   float* s_true;        // [nq]
   int64_t* true_id;     // [nq]
   int32_t* gt;          // [nq]
-  int32_t* eq;          // [nq]
-  int64_t* ranks;
-  int32_t* ties;
+  const uint32_t* fbits;  // [nq, W] excluded candidates (filtered ids + the true id)
+  int64_t W;
+  RankWin win;
   int32_t* err;
-  int prep_only;        // launch k_rank_prep only (the MFMA path counts on its own)
+  int prep_only;        // launch k_rank_prep only (the MFMA / tile paths count on their own)
+};
+
+// Reference-order refinement (k_rank_window / k_rank_refine / k_rank_exact).
+struct RefArgs {
+  const float* ent;
+  const float* rel;
+  const float* modulus;
+  const int64_t* queries;
+  int64_t nq, E, R;
+  int Le, Lr, K;           // K = reduction length (complex: Le / 2)
+  Consts c;
+  const float* q;          // [nq, Le] fast-path q (k_rank_prep)
+  float* qref;             // [nq, Le] reference-order q
+  const int64_t* true_id;  // [nq]
+  const float* s_true;     // [nq] fast-path true score
+  float* sref_true;        // [nq] reference-order true score
+  float* delta;            // [nq] window
+  const float* stats;      // [2] max row L2 norm, max |x| of the entity table
+  int exact_fast;          // the fast pass is already in reference order (TransE on the register tile)
+  const int32_t* ucnt;
+  const int32_t* ulist;
+  int cap;
+  const uint32_t* fbits;
+  int64_t W;
+  int32_t* gt;             // += refined strictly-greater
+  int32_t* eq;             // += refined ties
+  int32_t* gtx;            // overflowed queries: exact counts over every candidate
+  int32_t* eqx;
+  int32_t* err;
 };
 
 // Register-tiled filtered ranking (kge_kernels.inc, k_rank_tile): 64 queries ×
@@ -146,7 +196,7 @@ struct TileArgs {
   const uint32_t* fbits;   // [nq, W] filtered-candidate bitmap
   int64_t W;
   int32_t* gt;             // [nq]
-  int32_t* eq;             // [nq]
+  RankWin win;
 };
 
 struct ModelOps {
@@ -155,6 +205,8 @@ struct ModelOps {
   int (*entity)(int mode, int vec, int ns, const EntArgs&, hipStream_t);
   int (*rank)(int mode, int vec, int ns, const RankArgs&, hipStream_t);
   int (*rank_tile)(int mode, int gather, const TileArgs&, hipStream_t);
+  // stage 0: window (δ, reference q); 1: refine the listed candidates; 2: exact rescan of overflowed queries
+  int (*rank_ref)(int mode, int stage, const RefArgs&, hipStream_t);
 };
 
 ModelOps model_ops_transe();

@@ -21,7 +21,9 @@
 // and a 2-word slice of the query's exclusion bitmap (filtered ids, the true
 // id, ids past E) with plain per-lane integer counts, adds the two lane halves,
 // and issues one LDS and then one global integer atomic per (block, query):
-// exact and order-free.
+// exact and order-free.  Candidates within the query's near-tie window are not
+// counted but listed (win_count) for the reference-order refinement
+// (kge_rank_ref.h): the fma order here is not the reference's sum order.
 #include "kge_common.h"
 
 namespace kge {
@@ -47,7 +49,7 @@ struct MfmaArgs {
   const uint32_t* fbits;   // [nq, W] filtered-candidate bitmap (scan pass)
   int64_t W;
   int32_t* gt;             // [nq]
-  int32_t* eq;             // [nq]
+  RankWin win;
 };
 
 // One [128 rows × BK] slab of row-major [*, K] data: thread t holds float4
@@ -91,8 +93,8 @@ __global__ __launch_bounds__(256, 3) void k_rank_mfma(MfmaArgs a) {
   __shared__ __attribute__((aligned(16))) float As[BM][LDK];
   __shared__ __attribute__((aligned(16))) float Bs[BN][LDK];
   __shared__ int64_t arow[128], brow[128];
-  __shared__ float sts[128];
-  __shared__ int32_t cgt[128], ceq[128];
+  __shared__ float sts[128], sdl[128];
+  __shared__ int32_t cgt[128];
   const int t = threadIdx.x, lane = t & 63, w = wave_id();
   const int wm = w >> 1, wn = w & 1;
   const int64_t q0 = (int64_t)blockIdx.y * BM;
@@ -107,9 +109,9 @@ __global__ __launch_bounds__(256, 3) void k_rank_mfma(MfmaArgs a) {
       const int64_t e = e0 + t;
       brow[t] = (e < a.E) ? e : -1;
       sts[t] = (q < a.nq) ? a.s_true[q] : 0.f;
+      sdl[t] = (q < a.nq) ? a.win.delta[q] : 0.f;
     }
     cgt[t] = 0;
-    ceq[t] = 0;
   }
   __syncthreads();
 
@@ -180,7 +182,7 @@ __global__ __launch_bounds__(256, 3) void k_rank_mfma(MfmaArgs a) {
   for (int j = 0; j < 2; ++j) {
     const int n = wn * 64 + j * 32 + li;
     const int64_t q = arow[n];
-    const float st = sts[n];
+    const float st = sts[n], dlt = sdl[n];
     // excluded candidates of this query among rows wm·64 .. +63: filtered ids
     // and the true id (bitmap), and ids past E
     uint32_t ex[2];
@@ -193,7 +195,7 @@ __global__ __launch_bounds__(256, 3) void k_rank_mfma(MfmaArgs a) {
       if (valid < 32) word |= (valid <= 0) ? ~0u : (~0u << valid);
       ex[i] = word;
     }
-    int g = 0, e_ = 0;
+    int g = 0;
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -201,22 +203,19 @@ __global__ __launch_bounds__(256, 3) void k_rank_mfma(MfmaArgs a) {
         const int mloc = (r & 3) + 8 * (r >> 2) + 4 * kh;
         const bool ok = ((ex[i] >> mloc) & 1u) == 0u;
         const float sc = acc[i][j][r];
-        g += (ok && sc > st) ? 1 : 0;
-        e_ += (ok && sc == st) ? 1 : 0;
+        const float diff = sc - st;
+        g += (ok && diff > dlt) ? 1 : 0;
+        if (ok && !(diff > dlt) && diff >= -dlt) {  // near tie: listed, not counted
+          const int idx = atomicAdd(&a.win.ucnt[q], 1);
+          if (idx < a.win.cap) a.win.ulist[q * (int64_t)a.win.cap + idx] = (int32_t)(e0 + wm * 64 + i * 32 + mloc);
+        }
       }
     // lanes l and l + 32 hold the two row halves of the same query column
     g += __shfl_xor(g, 32);
-    e_ += __shfl_xor(e_, 32);
-    if (kh == 0 && q >= 0) {
-      if (g) atomicAdd(&cgt[n], g);
-      if (e_) atomicAdd(&ceq[n], e_);
-    }
+    if (kh == 0 && q >= 0 && g) atomicAdd(&cgt[n], g);
   }
   __syncthreads();
-  if (t < 128 && arow[t] >= 0) {
-    if (cgt[t]) atomicAdd(&a.gt[q0 + t], cgt[t]);
-    if (ceq[t]) atomicAdd(&a.eq[q0 + t], ceq[t]);
-  }
+  if (t < 128 && arow[t] >= 0 && cgt[t]) atomicAdd(&a.gt[q0 + t], cgt[t]);
 }
 
 // filtered-candidate bitmap from the CSR (one thread per filtered id)
@@ -240,14 +239,16 @@ __global__ __launch_bounds__(256) void k_filter_bits(const int64_t* __restrict__
   }
 }
 
-__global__ __launch_bounds__(256) void k_rank_emit(const int32_t* __restrict__ gt, const int32_t* __restrict__ eq,
-                                                   const int64_t* __restrict__ true_id, int64_t nq,
-                                                   int64_t* __restrict__ ranks, int32_t* __restrict__ ties) {
+// rank = 1 + #{strictly greater} (counted beyond the window + refined inside
+// it), or the exact rescan's count for an overflowed window
+__global__ __launch_bounds__(256) void k_rank_emit(EmitArgs a) {
   const int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (q >= nq) return;
-  const bool ok = true_id[q] >= 0;
-  ranks[q] = ok ? 1 + (int64_t)gt[q] : 0;
-  if (ties) ties[q] = ok ? eq[q] : 0;
+  if (q >= a.nq) return;
+  const bool ok = a.true_id[q] >= 0;
+  const bool ovf = a.ucnt[q] > a.cap;
+  a.ranks[q] = ok ? 1 + (int64_t)(ovf ? a.gtx[q] : a.gt[q]) : 0;
+  if (a.ties) a.ties[q] = ok ? (ovf ? a.eqx[q] : a.eq[q]) : 0;
+  if (a.listed) a.listed[q] = ok ? a.ucnt[q] : 0;
 }
 
 }  // namespace
@@ -263,32 +264,61 @@ int launch_filter_bits(const int64_t* filt_off, const int64_t* filt_ids, const i
   return (int)hipGetLastError();
 }
 
-int launch_rank_emit(const int32_t* gt, const int32_t* eq, const int64_t* true_id, int64_t nq, int64_t* ranks,
-                     int32_t* ties, hipStream_t s) {
-  hipLaunchKernelGGL(k_rank_emit, dim3((unsigned)((nq + 255) / 256)), dim3(256), 0, s, gt, eq, true_id, nq, ranks,
-                     ties);
+int launch_rank_emit(const EmitArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(k_rank_emit, dim3((unsigned)((a.nq + 255) / 256)), dim3(256), 0, s, a);
   return (int)hipGetLastError();
 }
 
-// q, true ids (and the q-prep's s_true slot) come from k_rank_prep.
-int launch_rank_mfma(const float* q, const float* ent, int64_t nq, int64_t E, int K, const int64_t* true_id,
-                     float* s_true, const int64_t* filt_off, const int64_t* filt_ids, uint32_t* bits, int32_t* gt,
-                     int32_t* eq, int64_t* ranks, int32_t* ties, int32_t* err, hipStream_t s) {
-  const int64_t W = (E + 31) / 32;
-  int st = launch_filter_bits(filt_off, filt_ids, true_id, nq, E, bits, err, s);
-  if (st) return st;
+// q and true ids come from k_rank_prep.  gather = 1: s_true (the queries'
+// true rows as the candidate block, diagonal kept); 0: the counting pass
+// against all E candidates, with the window from k_rank_window.
+int launch_rank_mfma(int gather, const float* q, const float* ent, int64_t nq, int64_t E, int K,
+                     const int64_t* true_id, float* s_true, const uint32_t* bits, int32_t* gt, const RankWin& win,
+                     hipStream_t s) {
   MfmaArgs a;
   a.q = q; a.ent = ent; a.nq = nq; a.E = E; a.K = K; a.true_id = true_id; a.s_true = s_true;
-  a.fbits = bits; a.W = W; a.gt = gt; a.eq = eq;
+  a.fbits = bits; a.W = (E + 31) / 32; a.gt = gt; a.win = win;
   const unsigned gy = (unsigned)((nq + BM - 1) / BM);
   // 3 waves/SIMD (158 VGPRs, no spills); 4 fits only with 13 spilled VGPRs
   // and measured 12 % slower
-  const dim3 gs((unsigned)((E + BN - 1) / BN), gy);
-  hipLaunchKernelGGL((k_rank_mfma<true>), dim3(1, gy), dim3(256), 0, s, a);
-  hipLaunchKernelGGL((k_rank_mfma<false>), gs, dim3(256), 0, s, a);
-  st = (int)hipGetLastError();
-  if (st) return st;
-  return launch_rank_emit(gt, eq, true_id, nq, ranks, ties, s);
+  if (gather) {
+    hipLaunchKernelGGL((k_rank_mfma<true>), dim3(1, gy), dim3(256), 0, s, a);
+  } else {
+    const dim3 gs((unsigned)((E + BN - 1) / BN), gy);
+    hipLaunchKernelGGL((k_rank_mfma<false>), gs, dim3(256), 0, s, a);
+  }
+  return (int)hipGetLastError();
+}
+
+// Entity-table statistics for the ranking windows: stats[0] = max row L2
+// norm, stats[1] = max |x| (non-negative floats order like their bit
+// patterns, so an integer atomicMax is exact).  One wave per row.
+__global__ __launch_bounds__(256) void k_table_stats(const float* __restrict__ ent, int64_t E, int Le,
+                                                     float* stats) {
+  const int lane = threadIdx.x & 63;
+  const int64_t e = (int64_t)blockIdx.x * 4 + wave_id();
+  if (e >= E) return;
+  const float* row = ent + e * Le;
+  float s2 = 0.f, mx = 0.f;
+  for (int k = lane; k < Le; k += 64) {
+    const float v = row[k];
+    s2 += v * v;
+    mx = fmaxf(mx, fabsf(v));
+  }
+  s2 = wave_sum(s2);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+  if (lane == 0) {
+    atomicMax(reinterpret_cast<unsigned int*>(&stats[0]), __float_as_uint(sqrtf(s2) * 1.0001f));
+    atomicMax(reinterpret_cast<unsigned int*>(&stats[1]), __float_as_uint(mx));
+  }
+}
+
+int launch_table_stats(const float* ent, int64_t E, int Le, float* stats, hipStream_t s) {
+  hipError_t e = hipMemsetAsync(stats, 0, 2 * sizeof(float), s);
+  if (e != hipSuccess) return (int)e;
+  hipLaunchKernelGGL(k_table_stats, dim3((unsigned)((E + 3) / 4)), dim3(256), 0, s, ent, E, Le, stats);
+  return (int)hipGetLastError();
 }
 
 }  // namespace kge

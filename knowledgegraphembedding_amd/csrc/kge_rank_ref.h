@@ -1,0 +1,155 @@
+// kge_rank_ref.h — reference-order scores for the ranking refinement.
+//
+// The fast ranking passes (MFMA tile, register tile, wave scan) sum a
+// candidate's terms in their own order, so a candidate whose fp32 score lies
+// within rounding distance of the true entity's can land on the other side of
+// it than in the reference.  Those candidates (a per-query window δ_q, see
+// k_rank_window) are re-scored here with the reference's own fp32 operation
+// sequence, which this file restates:
+//
+//  * the per-element ops of model.py:166-249 as separate IEEE operations
+//    (each ATen op rounds once; the build has -ffp-contract=off; RotatE's
+//    stack(...).norm(dim=0) evaluates sqrt(fma(im, im, re*re)) — pinned on the
+//    reference's output, tests/golden/make_golden.py `gen_rank_order`);
+//  * ATen's CPU `sum(dim=2)` over the contiguous last dim (SumKernel's
+//    vectorized_inner_sum / row_sum / multi_row_sum, 8-float vectors, 4
+//    interleaved accumulators with the 4-level cascade) for DistMult, ComplEx,
+//    RotatE and pRotatE;
+//  * `torch.norm(p=1, dim=2)` as a sequential fp32 sum for TransE.
+//
+// Every fp32 operation matches the reference bit for bit, except RotatE's
+// cos/sin and pRotatE's sin: the reference's vectorized CPU transcendentals
+// are not reproducible here; these use correctly rounded values (double
+// evaluation rounded once), which differ from the reference's in the last
+// bit for a few percent of arguments.
+#pragma once
+#include "kge_device.h"
+
+namespace kge {
+
+// correctly rounded fp32 transcendentals (a double result rounded once)
+__device__ __forceinline__ float sin_rn(float x) { return (float)sin((double)x); }
+__device__ __forceinline__ float cos_rn(float x) { return (float)cos((double)x); }
+__device__ __forceinline__ float sqrt_rn(float x) { return __fsqrt_rn(x); }
+
+// reference q for one element (model.py association; RotatE trig rounded once)
+template <int M, int MODE>
+__device__ __forceinline__ void ref_make_q(float xa, float xb, float ra, float rb, const Consts& c, float& qa,
+                                           float& qb) {
+  if constexpr (M == ROTATE) {
+    const float th = ra / c.kappa;
+    const float cs = cos_rn(th), sn = sin_rn(th);
+    if constexpr (MODE == HEAD_BATCH) {  // re_r·re_t + im_r·im_t ; re_r·im_t − im_r·re_t
+      qa = cs * xa + sn * xb;
+      qb = cs * xb - sn * xa;
+    } else {                             // re_h·re_r − im_h·im_r ; re_h·im_r + im_h·re_r
+      qa = xa * cs - xb * sn;
+      qb = xa * sn + xb * cs;
+    }
+  } else {
+    Elem<M, MODE>::make_q(xa, xb, ra, rb, c, qa, qb);  // exact already: no transcendentals
+  }
+}
+
+// one element of the [B, E, K] tensor the reference reduces over dim 2
+template <int M, int MODE>
+__device__ __forceinline__ float ref_elem(float qa, float qb, float ea, float eb, const Consts& c) {
+  constexpr bool HEAD = (MODE == HEAD_BATCH);
+  if constexpr (M == TRANSE) {
+    return fabsf(HEAD ? (ea + qa) : (qa - ea));
+  } else if constexpr (M == DISTMULT) {
+    return HEAD ? (ea * qa) : (qa * ea);
+  } else if constexpr (M == COMPLEX) {
+    return HEAD ? (ea * qa + eb * qb) : (qa * ea + qb * eb);
+  } else if constexpr (M == ROTATE) {
+    const float re = qa - ea, im = qb - eb;
+    return sqrt_rn(__builtin_fmaf(im, im, re * re));
+  } else {
+    const float pe = ea / c.kappa_p;
+    return fabsf(sin_rn(HEAD ? (pe + qa) : (qa - pe)));
+  }
+}
+
+template <int M>
+__device__ __forceinline__ float ref_finish(float total, const Consts& c) {
+  if constexpr (M == TRANSE || M == ROTATE) return c.gamma - total;
+  else if constexpr (M == PROTATE) return c.gamma - total * c.modulus;
+  else return total;
+}
+
+__host__ __device__ inline int ceil_log2_i(int64_t x) {
+  int r = 0;
+  while (((int64_t)1 << r) < x) ++r;
+  return r;
+}
+
+// Shuffle inside the caller's 32-lane half of the wave.
+__device__ __forceinline__ float half_shfl(float v, int src_hl) {
+  const int base = threadIdx.x & 32;
+  return __int_as_float(__builtin_amdgcn_ds_bpermute((base + src_hl) << 2, __float_as_int(v)));
+}
+
+// Reference-order score of the candidate row e against the query's reference
+// q, computed by one 32-lane half-wave (hl = lane within the half); every
+// lane of the half returns the score.  q / e: [K] real, or [re K | im K].
+template <int M, int MODE>
+__device__ float ref_score_half(const float* __restrict__ q, const float* __restrict__ e, int K, const Consts& c,
+                                int hl) {
+  constexpr bool CPLX = Traits<M>::cplx;
+  auto elem = [&](int k) -> float {
+    const float qa = q[k], ea = e[k];
+    const float qb = CPLX ? q[K + k] : 0.f, eb = CPLX ? e[K + k] : 0.f;
+    return ref_elem<M, MODE>(qa, qb, ea, eb, c);
+  };
+  if constexpr (M == TRANSE) {
+    // torch.norm(p=1): one fp32 accumulator, ascending k.  Lanes compute 32
+    // elements at a time; lane 0 adds them in order.
+    float acc = 0.f;
+    for (int k0 = 0; k0 < K; k0 += 32) {
+      const int k = k0 + hl;
+      const float v = (k < K) ? elem(k) : 0.f;
+      const int m = (K - k0 < 32) ? (K - k0) : 32;
+      for (int j = 0; j < m; ++j) acc += half_shfl(v, j);
+    }
+    return ref_finish<M>(acc, c);
+  } else {
+    // ATen sum(dim=2): 8-float vectors; vector v = 4·row + col over
+    // size_ilp = ⌊(K/8)/4⌋ rows (multi_row_sum, cascade levels of 2^lp rows),
+    // tail vectors into column 0, columns folded 0+1+2+3, then the scalar
+    // tail k ≥ 8·⌊K/8⌋ summed from 0 and the 8 vector lanes added in order.
+    // Lane hl = 8·col + p owns elements 32·row + hl.
+    const int nvec = K / 8;
+    const int size = nvec / 4;
+    const int lp0 = ceil_log2_i(size) / 4;
+    const int lp = lp0 > 4 ? lp0 : 4;
+    const int step = 1 << lp;
+    const int64_t mask = step - 1;
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+    int i = 0;
+    while (i + step <= size) {
+      for (int j = 0; j < step; ++j, ++i) acc[0] += elem(32 * i + hl);
+#pragma unroll
+      for (int lv = 1; lv < 4; ++lv) {
+        acc[lv] += acc[lv - 1];
+        acc[lv - 1] = 0.f;
+        if ((i & (mask << (lv * lp))) != 0) break;
+      }
+    }
+    for (; i < size; ++i) acc[0] += elem(32 * i + hl);
+    float col = acc[0];
+#pragma unroll
+    for (int lv = 1; lv < 4; ++lv) col += acc[lv];
+    if (hl < 8)
+      for (int v = 4 * size; v < nvec; ++v) col += elem(8 * v + hl);
+    const float c1 = half_shfl(col, (hl + 8) & 31), c2 = half_shfl(col, (hl + 16) & 31),
+                c3 = half_shfl(col, (hl + 24) & 31);
+    const float vacc = ((col + c1) + c2) + c3;  // valid in lanes 0..7
+    float fin = 0.f;
+    for (int k = 8 * nvec; k < K; ++k) fin += elem(k);
+#pragma unroll
+    for (int p = 0; p < 8; ++p) fin += half_shfl(vacc, p);
+    return ref_finish<M>(fin, c);
+  }
+}
+
+}  // namespace kge

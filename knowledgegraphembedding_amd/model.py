@@ -504,17 +504,18 @@ class KGEModel(nn.Module):
             'HITS@10': sum(1.0 if r <= 10 else 0.0 for r in ranks_seq) / n,
         }
 
-    def rank_queries(self, triples, all_true_triples, mode):
+    def rank_queries(self, triples, all_true_triples, mode, path="auto", listed=False):
         """Per-query filtered ranks and tie counts (numpy int64, int32) — the
-        quantity test_step averages; exposed for parity tests and tools."""
+        quantity test_step averages; exposed for parity tests and tools.
+        `path` / `listed`: see ops.rank_filtered."""
         dev = ops._require_device(self.entity_embedding)
         index = all_true_triples if isinstance(all_true_triples, FilterIndex) else \
             FilterIndex(all_true_triples, self.nentity, self.nrelation)
         q = np.asarray(triples, dtype=np.int64).reshape(-1, 3)
         off, ids = index.filter_csr(q, mode)
         with torch.no_grad():
-            ranks, ties = ops.rank_filtered(self.desc(), mode, torch.from_numpy(q), torch.from_numpy(off),
-                                            torch.from_numpy(ids), dev)
-        r, t = ranks.cpu().numpy(), ties.cpu().numpy()
+            out = ops.rank_filtered(self.desc(), mode, torch.from_numpy(q), torch.from_numpy(off),
+                                    torch.from_numpy(ids), dev, path=path, listed=listed)
+        res = tuple(t.cpu().numpy() for t in out)
         ops.raise_on_device_error(dev)
-        return r, t
+        return res

@@ -331,28 +331,38 @@ def adam_step(param: torch.Tensor, grad: torch.Tensor, exp_avg: torch.Tensor, ex
     )
 
 
+RANK_PATHS = {"auto": 0, "mfma": 1, "tile": 2, "scan": 3}
+
+
 def rank_filtered(desc: _lib.ModelDesc, mode: str, queries: torch.Tensor, filt_off: torch.Tensor,
-                  filt_ids: torch.Tensor, dev):
-    """Filtered ranks (int64) and tie counts for a block of queries (model.py:383-418)."""
+                  filt_ids: torch.Tensor, dev, path: str = "auto", listed: bool = False):
+    """Filtered ranks (int64) and tie counts (int32) for a block of queries
+    (model.py:383-418), in the reference's fp32 score order
+    (kge_rank_filtered_ex).  `path` picks the fast counting pass ("auto",
+    "mfma", "tile", "scan"); `listed` also returns the per-query number of
+    near-ties that were re-scored."""
     if mode not in ("head-batch", "tail-batch"):
         raise ValueError("mode %s not supported" % mode)
+    if path not in RANK_PATHS:
+        raise ValueError("rank path %s not supported" % path)
     q = _idx(queries, dev)
     off = _idx(filt_off, dev)
     ids = _idx(filt_ids, dev) if filt_ids.numel() else torch.zeros(1, dtype=torch.int64, device=dev)
     nq = q.shape[0]
     ranks = torch.empty(nq, dtype=torch.int64, device=dev)
     ties = torch.empty(nq, dtype=torch.int32, device=dev)
+    lst = torch.empty(nq, dtype=torch.int32, device=dev) if listed else None
     lib = _lib.load()
     need = lib.kge_rank_workspace_bytes(desc, nq)
     st = state(dev)
     ws = st.workspace(need)
     _lib.check(
-        lib.kge_rank_filtered(desc, _lib.MODE_IDS[mode], q.data_ptr(), nq, off.data_ptr(), ids.data_ptr(),
-                              ranks.data_ptr(), ties.data_ptr(), ws.data_ptr(), ws.numel(), st.err.data_ptr(),
-                              _stream(dev)),
-        "kge_rank_filtered",
+        lib.kge_rank_filtered_ex(desc, _lib.MODE_IDS[mode], q.data_ptr(), nq, off.data_ptr(), ids.data_ptr(),
+                                 ranks.data_ptr(), ties.data_ptr(), _ptr(lst), RANK_PATHS[path], ws.data_ptr(),
+                                 ws.numel(), st.err.data_ptr(), _stream(dev)),
+        "kge_rank_filtered_ex",
     )
-    return ranks, ties
+    return (ranks, ties, lst) if listed else (ranks, ties)
 
 
 def sample_negatives(triples: torch.Tensor, batch: torch.Tensor, nentity: int, negative_sample_size: int,

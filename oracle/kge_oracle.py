@@ -280,3 +280,106 @@ def sample_negatives(triples, batch, nentity: int, n: int, mode: str, key: int, 
         take = got[:n]
         neg[i, :len(take)] = take
     return pos, neg, ok
+
+
+# ------------------------------------- reference operation order (numpy)
+# The sequence of fp32 operations the reference's CPU forward performs,
+# written out element by element — what the HIP ranking refinement
+# (csrc/kge_rank_ref.h) reproduces.  Pinned by tests/test_oracle_golden.py
+# against the golden scores the reference itself produced (bit for bit).
+U32 = np.float32
+
+
+def aten_sum_lastdim(x: np.ndarray) -> np.ndarray:
+    """ATen CPU `sum(dim=-1)` of a contiguous fp32 array, in its own order
+    (SumKernel.cpp vectorized_inner_sum → row_sum → multi_row_sum: 8-float
+    vectors, 4 interleaved accumulators, a 4-level cascade of 2^lp rows, tail
+    vectors into accumulator 0, then the scalar tail from 0 and the 8 vector
+    lanes in order).  Requires the last dim >= 8."""
+    x = np.ascontiguousarray(x, dtype=np.float32)
+    d = x.shape[-1]
+    nvec = d // 8
+    vecs = np.moveaxis(x[..., :nvec * 8].reshape(x.shape[:-1] + (nvec, 8)), -2, 0)  # [nvec, ..., 8]
+    size = nvec // 4
+    rows = vecs[:size * 4].reshape((size, 4) + vecs.shape[1:])
+    lp = max(4, (int(np.ceil(np.log2(size))) if size > 1 else 0) // 4)
+    step, mask = 1 << lp, (1 << lp) - 1
+    acc = np.zeros((4, 4) + vecs.shape[1:], np.float32)  # [level, column, ..., 8]
+    i = 0
+    while i + step <= size:
+        for _ in range(step):
+            acc[0] = acc[0] + rows[i]
+            i += 1
+        for lv in range(1, 4):
+            acc[lv] = acc[lv] + acc[lv - 1]
+            acc[lv - 1] = 0
+            if i & (mask << (lv * lp)):
+                break
+    while i < size:
+        acc[0] = acc[0] + rows[i]
+        i += 1
+    cols = acc[0]
+    for lv in range(1, 4):
+        cols = cols + acc[lv]
+    ps0 = cols[0]
+    for v in range(size * 4, nvec):
+        ps0 = ps0 + vecs[v]
+    vacc = ps0
+    for k in range(1, 4):
+        vacc = vacc + cols[k]
+    fin = np.zeros(x.shape[:-1], np.float32)
+    for k in range(nvec * 8, d):
+        fin = fin + x[..., k]
+    for p in range(8):
+        fin = fin + vacc[..., p]
+    return fin
+
+
+def ref_order_scores(name: str, ent: np.ndarray, rel: np.ndarray, modulus, sample, mode: str, gamma: float,
+                     erange: float, trig=None) -> np.ndarray:
+    """Scores of KGEModel.forward (model.py:72-249) as explicit fp32 element
+    operations + aten_sum_lastdim / a sequential L1 sum.  `trig` (cos, sin)
+    evaluates the transcendentals; default: torch's CPU ones (the reference's)."""
+    cos, sin = trig or ((lambda a: torch.cos(torch.from_numpy(np.array(a, np.float32))).numpy()),
+                        (lambda a: torch.sin(torch.from_numpy(np.array(a, np.float32))).numpy()))
+    h, r, t = (a.numpy() for a in gather(torch.from_numpy(ent), torch.from_numpy(rel), sample, mode))
+    head = mode == 'head-batch'
+    g = U32(gamma)
+    if name == 'TransE':
+        x = np.abs(h + (r - t) if head else (h + r) - t)
+        acc = np.zeros(x.shape[:-1], np.float32)
+        for k in range(x.shape[-1]):
+            acc = acc + x[..., k]
+        return g - acc
+    if name == 'DistMult':
+        return aten_sum_lastdim(h * (r * t) if head else (h * r) * t)
+    if name == 'ComplEx':
+        hr, hi = np.split(h, 2, axis=2)
+        rr, ri = np.split(r, 2, axis=2)
+        tr, ti = np.split(t, 2, axis=2)
+        if head:
+            a, b = rr * tr + ri * ti, rr * ti - ri * tr
+            x = hr * a + hi * b
+        else:
+            a, b = hr * rr - hi * ri, hr * ri + hi * rr
+            x = a * tr + b * ti
+        return aten_sum_lastdim(x)
+    if name == 'RotatE':
+        hr, hi = np.split(h, 2, axis=2)
+        tr, ti = np.split(t, 2, axis=2)
+        ph = r / U32(erange / PI)
+        cr, sr = cos(ph), sin(ph)
+        if head:
+            re, im = (cr * tr + sr * ti) - hr, (cr * ti - sr * tr) - hi
+        else:
+            re, im = (hr * cr - hi * sr) - tr, (hr * sr + hi * cr) - ti
+        re, im = np.broadcast_arrays(re, im)
+        el = np.sqrt((im.astype(np.float64) * im + (re * re).astype(np.float64)).astype(np.float32))
+        return g - aten_sum_lastdim(el)
+    if name == 'pRotatE':
+        div = U32(erange / PI_PROTATE)
+        ph, pr, pt = h / div, r / div, t / div
+        x = ph + (pr - pt) if head else (ph + pr) - pt
+        return g - aten_sum_lastdim(np.abs(sin(np.ascontiguousarray(np.broadcast_to(x, np.broadcast_shapes(
+            ph.shape, pr.shape, pt.shape)))))) * U32(modulus.reshape(-1)[0])
+    raise ValueError('model %s not supported' % name)

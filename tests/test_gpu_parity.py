@@ -3,8 +3,7 @@
 Tolerances (north star):
   scores / losses:  |Δ| ≤ 1e-4 · max(|s_ref|, 1)
   gradients:        |Δ| ≤ 1e-4 · max|g_ref| + 1e-4 · |g_ref|  (fp32 sums in another order)
-  ranks:            bit-exact on every query whose fp64 margin exceeds 1e-4·max(|s|,1);
-                    tie / near-tie queries are reported, and must stay within [count, count+ties]
+  ranks:            tests/test_rank_parity_gpu.py
 """
 from argparse import Namespace
 
@@ -338,65 +337,7 @@ def test_kge_adam_matches_torch_adam():
 
 
 # ------------------------------------------------------------------ ranking
-# default: MFMA tile (DistMult/ComplEx) + register tile (distance models);
-# tile: the register tile for every model; scan: the per-pair wave-reduction scan
-RANK_PATHS = {"default": {}, "tile": {"KGE_RANK_MFMA": "0"}, "scan": {"KGE_RANK_MFMA": "0", "KGE_RANK_TILE": "0"}}
-
-
-@pytest.mark.parametrize("path", list(RANK_PATHS))
-def test_ranks_vs_golden(g_ranks, golden_info, path, monkeypatch):
-    for k, v in RANK_PATHS[path].items():
-        monkeypatch.setenv(k, v)
-    report = []
-    for kg in golden_info["ranks"]:
-        tag, E, R, d, seed = kg["tag"], kg["E"], kg["R"], kg["d"], kg["seed"]
-        all_true = g_ranks[f"{tag}/all_true"]
-        test = g_ranks[f"{tag}/test"]
-        for name in kg["models"]:
-            m, ent, rel, mod, rng = build_model(name, E, R, d, kg["gamma"], seed)
-            g = torch.Tensor([kg["gamma"]]).item()
-            for mode in ("head-batch", "tail-batch"):
-                ranks, ties = m.rank_queries(test, all_true, mode)
-                ref = g_ranks[f"{tag}/{name}/{mode}/rank"]
-                orc = O.filtered_ranks(name, torch.from_numpy(ent), torch.from_numpy(rel),
-                                       None if mod is None else torch.from_numpy(mod), test, all_true, mode, g, rng)
-                # exact-rank claim: every query whose fp64 margin exceeds the fp32
-                # score tolerance 1e-4·max(|s|, 1) and that has no exact tie
-                clear = (orc["margin64"] > 1e-4 * np.maximum(1.0, np.abs(orc["score64"]))) & (ties == 0)
-                mism = (ranks != ref) & clear
-                assert not mism.any(), f"{tag} {name} {mode}: {np.nonzero(mism)[0]} {ranks[mism]} vs {ref[mism]}"
-                report.append((tag, name, mode, int(clear.sum()), int((~clear).sum()),
-                               int((ranks == ref).sum()), len(ref)))
-    print("rank parity (tag, model, mode, clear, ambiguous, exact, total):")
-    for r in report:
-        print("  ", r)
-
-
-def test_protate_tile_ranks_vs_oracle_and_scan(monkeypatch):
-    """pRotatE's register tile scores sin(q − e) / sin(e + q) by the
-    angle-difference identity from staged (sin, cos) pairs.  Its ranks must
-    equal the oracle's strict-count rank on every query whose fp64 margin clears
-    the fp32 score tolerance, and the sinf-based wave scan (KGE_RANK_TILE=0) on
-    the same queries; E = 300 keeps most score gaps above that tolerance."""
-    E, R, d, gamma = 300, 7, 64, 12.0
-    m, ent, rel, mod, rng = build_model("pRotatE", E, R, d, gamma, 11)
-    rs = np.random.RandomState(5)
-    true = np.unique(np.stack([rs.randint(0, E, 900), rs.randint(0, R, 900), rs.randint(0, E, 900)], 1), axis=0)
-    test = true[rs.randint(0, len(true), 48)]
-    g = torch.Tensor([gamma]).item()
-    clear_total = 0
-    for mode in ("head-batch", "tail-batch"):
-        monkeypatch.setenv("KGE_RANK_TILE", "1")
-        tile, ties = m.rank_queries(test, true, mode)
-        monkeypatch.setenv("KGE_RANK_TILE", "0")
-        scan, _ = m.rank_queries(test, true, mode)
-        orc = O.filtered_ranks("pRotatE", torch.from_numpy(ent), torch.from_numpy(rel),
-                               None if mod is None else torch.from_numpy(mod), test, true, mode, g, rng)
-        clear = (orc["margin64"] > 1e-4 * np.maximum(1.0, np.abs(orc["score64"]))) & (ties == 0)
-        clear_total += int(clear.sum())
-        assert np.array_equal(tile[clear], orc["rank_count"][clear]), mode
-        assert np.array_equal(tile[clear], scan[clear]), mode
-    assert clear_total >= 30, clear_total
+# rank parity with the reference: tests/test_rank_parity_gpu.py
 
 
 def test_test_step_metrics_vs_golden(g_ranks, golden_info):

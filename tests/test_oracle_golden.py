@@ -32,6 +32,39 @@ def test_oracle_scores(g_scores, tag, E, R, d, B, n, gamma, seed, name):
         np.testing.assert_allclose(s, ref, rtol=2e-6, atol=2e-6 * max(1.0, np.abs(ref).max()))
 
 
+@pytest.mark.parametrize("tag,E,R,d,B,n,gamma,seed", [("small", 64, 8, 16, 4, 8, 12.0, 11),
+                                                       ("d1000", 128, 16, 1000, 8, 16, 24.0, 12)])
+@pytest.mark.parametrize("name", ["TransE", "DistMult", "ComplEx", "RotatE", "pRotatE"])
+def test_reference_operation_order(g_scores, tag, E, R, d, B, n, gamma, seed, name):
+    """The element-by-element restatement of the reference's fp32 operations
+    (O.ref_order_scores: ATen's sum(dim=2) order, torch.norm(p=1)'s sequential
+    sum, RotatE's sqrt(fma(im, im, re*re))) reproduces the reference's golden
+    scores BIT FOR BIT — the order the HIP ranking refinement implements
+    (csrc/kge_rank_ref.h).  The transcendentals here are torch's, as in the
+    reference; the kernels round cos/sin correctly instead."""
+    if torch.backends.cpu.get_cpu_capability() not in ("AVX2", "AVX512"):
+        pytest.skip("the golden scores were made with AVX2/AVX512 ATen kernels")
+    ent, rel, mod, rng = synth_tables(name, E, R, d, gamma, seed)
+    pos, neg, _ = synth.kge_batch(seed, B, n, E, R)
+    P, N = torch.from_numpy(pos), torch.from_numpy(neg)
+    g = torch.Tensor([gamma]).item()
+    for mode in MODES:
+        s = O.ref_order_scores(name, ent, rel, mod, P if mode == "single" else (P, N), mode, g, rng)
+        ref = g_scores[f"{tag}/{name}/{mode}"]
+        assert s.dtype == np.float32 and s.shape == ref.shape
+        np.testing.assert_array_equal(s.view(np.int32), ref.view(np.int32), err_msg=f"{name} {mode}")
+
+
+@pytest.mark.parametrize("d", [8, 9, 15, 16, 17, 31, 100, 127, 128, 500, 511, 512, 1000, 2000, 4100])
+def test_aten_sum_order(d):
+    """O.aten_sum_lastdim is torch's CPU sum(dim=-1), bit for bit, for every
+    tail shape (scalar tail, vector tail, partial and full cascade blocks)."""
+    if torch.backends.cpu.get_cpu_capability() not in ("AVX2", "AVX512"):
+        pytest.skip("order restated for the AVX2/AVX512 ATen kernels")
+    x = (np.random.default_rng(d).standard_normal((37, d)) * 0.01).astype(np.float32)
+    np.testing.assert_array_equal(O.aten_sum_lastdim(x).view(np.int32), torch.from_numpy(x).sum(-1).numpy().view(np.int32))
+
+
 def test_oracle_train(g_train, golden_info):
     ti = golden_info["train"]
     E, R, d, B, n, gamma, seed = ti["E"], ti["R"], ti["d"], ti["B"], ti["n"], ti["gamma"], ti["seed"]
