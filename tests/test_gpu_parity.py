@@ -365,6 +365,46 @@ def test_countries_auc_pr(g_countries, golden_info):
 
 
 # ------------------------------------------------------------- full size
+@pytest.mark.parametrize("mode", ["tail-batch", "head-batch"])
+def test_config2_full_shape_grads_vs_oracle(mode):
+    """The benchmarked launch shapes (RotatE FB15k, B = 1024, n = 256, d = 1000
+    -adv, Σw subsampling: the 4-slice entity pass with its LDS budget, 1024
+    row blocks) against the oracle's autograd of the reference's op chain:
+    the three losses, every relation-gradient row and 512 sampled entity-
+    gradient rows (all rows each sampled entity occurs in are included — the
+    oracle runs the whole batch, in 128-row chunks whose gradients are
+    re-weighted by Σw_chunk / Σw, the reference's loss being linear in them)."""
+    E, R, d, B, n, gamma = 14951, 1345, 1000, 1024, 256, 24.0
+    m, ent, rel, mod, rng = build_model("RotatE", E, R, d, gamma, 0)
+    pos, neg, w = synth.kge_batch(2, B, n, E, R)
+    args = Namespace(negative_adversarial_sampling=True, adversarial_temperature=1.0, uni_weight=False,
+                     regularization=0.0)
+    losses = m.compute_train_grads(torch.from_numpy(pos).to(DEV), torch.from_numpy(neg).to(DEV),
+                                   torch.from_numpy(w).to(DEV), mode, args).cpu().numpy()
+    ge = m.entity_embedding.grad.cpu().numpy()
+    gr = m.relation_embedding.grad.cpu().numpy()
+    ops.raise_on_device_error(DEV)
+    torch.set_num_threads(max(1, min(16, len(__import__("os").sched_getaffinity(0)))))
+    E_, R_ = torch.from_numpy(ent), torch.from_numpy(rel)
+    wsum = float(np.float64(w.astype(np.float64).sum()))
+    ref_l = np.zeros(3)
+    ref_ge = np.zeros_like(ent, dtype=np.float64)
+    ref_gr = np.zeros_like(rel, dtype=np.float64)
+    for c0 in range(0, B, 128):
+        sl = slice(c0, c0 + 128)
+        log, cge, cgr, _ = O.train_grads("RotatE", E_, R_, None, torch.from_numpy(pos[sl]), torch.from_numpy(neg[sl]),
+                                         torch.from_numpy(w[sl]), mode, adversarial=True, temperature=1.0,
+                                         uni_weight=False, regularization=0.0, gamma=gamma, erange=rng)
+        f = float(w[sl].astype(np.float64).sum()) / wsum
+        ref_l += f * np.array([log["positive_sample_loss"], log["negative_sample_loss"], log["loss"]])
+        ref_ge += f * cge.numpy()
+        ref_gr += f * cgr.numpy()
+    assert np.all(np.abs(losses[:3] - ref_l) <= 1e-4 * np.maximum(1, np.abs(ref_l))), (losses[:3], ref_l)
+    rows = np.unique(np.concatenate([synth.randint(5, (384,), E), pos[:64, 0], pos[:64, 2]]))
+    assert_close_grad(ge[rows], ref_ge[rows].astype(np.float32), f"entity rows ({mode})")
+    assert_close_grad(gr, ref_gr.astype(np.float32), f"relation rows ({mode})")
+
+
 def test_config2_full_size_properties():
     """BASELINE config 2 shape (RotatE FB15k d=1000 b=1024 n=256 -adv): finite,
     deterministic, and sampled rows equal to the oracle."""
