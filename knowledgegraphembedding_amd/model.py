@@ -22,34 +22,10 @@ import numpy as np
 import torch
 import torch.nn as nn
 
-from . import _lib, ops
+from . import _lib, ops, torch_ops  # noqa: F401  (torch_ops registers torch.ops.kge.*)
 from .filters import FilterIndex
 
 _MODELS = ['TransE', 'DistMult', 'ComplEx', 'RotatE', 'pRotatE']
-
-
-class _TableScore(torch.autograd.Function):
-    """score = kge_score(tables, indices); backward = kge_score_backward (dense grads)."""
-
-    @staticmethod
-    def forward(ctx, entity, relation, modulus, pos, neg, mode, name, gamma, erange):
-        dev = ops._require_device(entity, relation, pos, neg if neg is not None else pos)
-        desc = ops.make_desc(name, entity.detach(), relation.detach(), gamma, erange,
-                             None if modulus is None else modulus.detach())
-        out = ops.score(desc, mode, pos, neg, dev)
-        ctx.save_for_backward(entity, relation, modulus if modulus is not None else entity.new_empty(0), pos,
-                              neg if neg is not None else pos.new_empty(0))
-        ctx.meta = (mode, name, gamma, erange, modulus is not None)
-        return out
-
-    @staticmethod
-    def backward(ctx, grad_out):
-        entity, relation, modulus, pos, neg = ctx.saved_tensors
-        mode, name, gamma, erange, has_mod = ctx.meta
-        dev = entity.device
-        desc = ops.make_desc(name, entity.detach(), relation.detach(), gamma, erange, modulus if has_mod else None)
-        ge, gr, gm = ops.score_backward(desc, mode, pos, None if mode == 'single' else neg, grad_out, dev, has_mod)
-        return ge, gr, (gm.view_as(modulus) if has_mod else None), None, None, None, None, None, None
 
 
 class StepLog(dict):
@@ -267,9 +243,8 @@ class KGEModel(nn.Module):
         pos = pos.to(dev)
         neg = None if neg is None else neg.to(dev)
         g, rng = self._host_scalars()
-        score = _TableScore.apply(self.entity_embedding, self.relation_embedding, self._modulus(), pos, neg, mode,
-                                  self.model_name, g, rng)
-        return score
+        return torch.ops.kge.score(self.entity_embedding, self.relation_embedding, pos, neg, mode, self.model_name,
+                                   g, rng, self._modulus())
 
     # ------------------------------------------------------- score plug-ins
     def _plugin(self, name, head, relation, tail, mode):
@@ -296,8 +271,8 @@ class KGEModel(nn.Module):
         else:
             raise ValueError('mode %s not supported' % mode)
         g, rng = self._host_scalars()
-        return _TableScore.apply(ent.contiguous(), relation.reshape(B, -1).contiguous(), self._modulus(), pos, neg,
-                                 mode, name, g, rng)
+        return torch.ops.kge.score(ent.contiguous(), relation.reshape(B, -1).contiguous(), pos, neg, mode, name, g,
+                                   rng, self._modulus())
 
     def TransE(self, head, relation, tail, mode):
         return self._plugin('TransE', head, relation, tail, mode)

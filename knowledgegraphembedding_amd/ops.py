@@ -43,17 +43,26 @@ def _stream(dev: torch.device) -> int:
 
 
 class _DeviceState:
-    """Per-device scratch: a growable workspace and the device error flag."""
+    """Per-device scratch: a growable workspace per HIP stream, and the device
+    error flag (written only by atomic OR, so streams may share it).
+
+    Calls enqueued on one stream use that stream's workspace, so work issued
+    from two torch streams at once never shares scratch memory; a workspace
+    is replaced (not resized in place) when a larger call comes, and the
+    caching allocator keeps the old block until the stream has moved past it."""
 
     def __init__(self, dev: torch.device):
         self.dev = dev
-        self.ws = torch.empty(0, dtype=torch.uint8, device=dev)
+        self.ws = {}
         self.err = torch.zeros(1, dtype=torch.int32, device=dev)
 
     def workspace(self, nbytes: int) -> torch.Tensor:
-        if self.ws.numel() < nbytes:
-            self.ws = torch.empty(int(nbytes * 1.25) + 4096, dtype=torch.uint8, device=self.dev)
-        return self.ws
+        s = torch.cuda.current_stream(self.dev)
+        key = s.cuda_stream
+        ws = self.ws.get(key)
+        if ws is None or ws.numel() < nbytes:
+            ws = self.ws[key] = torch.empty(int(nbytes * 1.25) + 4096, dtype=torch.uint8, device=self.dev)
+        return ws
 
 
 _STATES: dict = {}
