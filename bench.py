@@ -260,9 +260,13 @@ def main():
     args = Namespace(cuda=True, negative_adversarial_sampling=True, adversarial_temperature=TEMP, uni_weight=False,
                      regularization=0.0, dp_group=group)
     part = None
-    if wl["partition"] and group is not None:
+    dp_mode = None if group is None else dp_exchange_mode(world)
+    if group is not None and (wl["partition"] or dp_mode == "owner"):
+        # config 5's row-partitioned table (KGE_PART_EXCHANGE, default the
+        # owner-computes "factors"), or the data-parallel "owner" exchange
         from knowledgegraphembedding_amd.partition import EntityRowPartition
-        part = EntityRowPartition(model, group)
+        exchange = os.environ.get("KGE_PART_EXCHANGE", "factors") if wl["partition"] else "factors"
+        part = EntityRowPartition(model, group, exchange=exchange)
         params = part.parameters()
     else:
         params = [p for p in model.parameters() if p.requires_grad]
@@ -342,11 +346,12 @@ def main():
         "dtype": "fp32",
         "data": "synthetic (uniform ids, U(-range,range) tables), batches pre-staged in HBM",
         "variant": {"fused_adam": model.fuse_optimizer, "keep_grads": model.keep_grads, "batches": sampler,
-                    "dp_exchange": (None if group is None or part is not None else dp_exchange_mode(world))},
+                    "dp_exchange": dp_mode,
+                    "partition_exchange": None if part is None else part.exchange},
         "config": {"workload": wl["name"],
                    "entities": E, "relations": R, "hidden_dim": D, "batch_per_gpu": B, "global_batch": B * world,
                    "negatives": NNEG, "adversarial_temperature": TEMP, "gamma": GAMMA,
-                   "parallelism": (f"rowpart{world}" if part is not None else f"dp{world}")},
+                   "parallelism": (f"rowpart{world}" if wl["partition"] and part is not None else f"dp{world}")},
         "stage_timed_steps": int(stage[6]),
         # HIP-event stage times of one step in TIMER_PERIOD, on the launching
         # stream; the CSR runs on a side stream beside the row pass, so these

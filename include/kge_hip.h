@@ -247,6 +247,27 @@ int kge_train_step_from_rows_csr(const kge_model_desc *m, int32_t mode, const in
                                  float *grad_modulus, float *losses_out, void *workspace, size_t workspace_bytes,
                                  int32_t *err_flag, void *stream);
 
+/*
+ * OWNER-COMPUTES step (partition.py, exchange "factors"): the rest of the step
+ * from the gathered factors, with the entity-major pass — gradient, fused Adam
+ * and regulariser — restricted to the caller's own rows [entity_begin,
+ * entity_end) of the global batch's occurrences; the relation pass, the
+ * positive epilogue and the losses cover the whole batch (identical on every
+ * rank).  adam->entity.exp_avg / exp_avg_sq may point `entity_begin` rows
+ * before the caller's shard-sized moment buffers (only owned rows are
+ * touched).  reg_relations = 0 leaves the relation rows out of the
+ * regularisation loss (another rank counts them); losses_out[3] then holds
+ * this rank's part.  csr_ready: the CSR was built by kge_train_csr.
+ */
+int kge_train_step_from_rows_range(const kge_model_desc *m, int32_t mode, const int64_t *pos, const int64_t *neg,
+                                   int64_t batch, int64_t nneg, const float *subsampling_weight,
+                                   const float *weight_sum, int32_t uni_weight, int64_t uni_batch,
+                                   float regularization, const float *g_in, const float *dq_in, float *stats_inout,
+                                   const kge_adam_desc *adam, float *grad_entity, float *grad_relation,
+                                   float *grad_modulus, float *losses_out, void *workspace, size_t workspace_bytes,
+                                   int32_t *err_flag, void *stream, int64_t entity_begin, int64_t entity_end,
+                                   int32_t csr_ready, int32_t reg_relations);
+
 
 /*
  * Σ subsampling_weight into *out (device scalar) — the denominator of

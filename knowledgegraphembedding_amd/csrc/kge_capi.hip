@@ -198,7 +198,7 @@ int run_grad(const kge_model_desc* m, const Geom& geo, int mode, const int64_t* 
              int64_t neg_stride, int64_t B, int64_t n, RowArgs ra, GradWs w, float* grad_entity,
              float* grad_relation, float* grad_modulus, float reg, FinArgs fa, const kge_adam_desc* adam,
              int32_t* err, hipStream_t s, int phases = KGE_PHASE_ALL, int64_t e_begin = 0, int64_t e_end = -1,
-             int xstage = XS_NONE) {
+             int xstage = XS_NONE, int reg_relations = 1) {
   const ModelOps& op = ops_for(m->model);
   AdamK ak;
   ak.b1 = adam ? adam->beta1 : 0.f;
@@ -364,7 +364,15 @@ int run_grad(const kge_model_desc* m, const Geom& geo, int mode, const int64_t* 
   }
   fa.row_stats = w.row_stats;
   fa.reg_partial = (reg != 0.f) ? w.reg_partial : nullptr;
-  fa.nreg = ent_parts + m->nrelation;
+  {
+    // entity rows [e_begin, e_end) (all of them unless an owner's range) and,
+    // unless the caller counts them elsewhere, the relation rows
+    const int64_t per = ent_parts / (m->nentity > 0 ? m->nentity : 1);
+    fa.reg_a0 = e_begin * per;
+    fa.reg_a1 = e_end * per;
+    fa.reg_b0 = ent_parts;
+    fa.reg_b1 = ent_parts + (reg_relations ? m->nrelation : 0);
+  }
   fa.regularization = reg;
   fa.grad_modulus = grad_modulus;
   fa.adam = adam_t((adam && m->model == KGE_PROTATE) ? &adam->modulus : nullptr);
@@ -500,7 +508,8 @@ static int train_impl(const kge_model_desc* m, int32_t mode, const int64_t* pos,
                       const kge_adam_desc* adam, float* grad_entity, float* grad_relation, float* grad_modulus,
                       float* losses_out, void* workspace, size_t workspace_bytes, int32_t* err_flag, void* stream,
                       int32_t phases = KGE_PHASE_ALL, int64_t e_begin = 0, int64_t e_end = -1, int xstage = XS_NONE,
-                      float* rows_g = nullptr, float* rows_dq = nullptr, float* rows_stats = nullptr) {
+                      float* rows_g = nullptr, float* rows_dq = nullptr, float* rows_stats = nullptr,
+                      int reg_relations = 1) {
   Geom geo;
   int st = check_model(m, &geo);
   if (st) return st;
@@ -563,7 +572,7 @@ static int train_impl(const kge_model_desc* m, int32_t mode, const int64_t* pos,
   if (e_begin < 0 || e_begin > e_end || e_end > m->nentity) return KGE_ERR_ARG;
   return run_grad(m, geo, mode, pos, neg, nneg, batch, nneg, ra, w, grad_entity, grad_relation,
                   m->model == KGE_PROTATE ? grad_modulus : nullptr, regularization, fa, adam, err_flag, s, phases,
-                  e_begin, e_end, xstage);
+                  e_begin, e_end, xstage, reg_relations);
 }
 
 int kge_train_rows_slice(const kge_model_desc* m, int32_t mode, const int64_t* pos, const int64_t* neg,
@@ -586,6 +595,22 @@ int kge_train_step_from_rows(const kge_model_desc* m, int32_t mode, const int64_
                     regularization, adam, grad_entity, grad_relation, grad_modulus, losses_out, workspace,
                     workspace_bytes, err_flag, stream, KGE_PHASE_ALL, 0, -1, XS_FROM_ROWS, const_cast<float*>(g_in),
                     const_cast<float*>(dq_in), stats_inout);
+}
+
+int kge_train_step_from_rows_range(const kge_model_desc* m, int32_t mode, const int64_t* pos, const int64_t* neg,
+                                   int64_t batch, int64_t nneg, const float* subsampling_weight,
+                                   const float* weight_sum, int32_t uni_weight, int64_t uni_batch,
+                                   float regularization, const float* g_in, const float* dq_in, float* stats_inout,
+                                   const kge_adam_desc* adam, float* grad_entity, float* grad_relation,
+                                   float* grad_modulus, float* losses_out, void* workspace, size_t workspace_bytes,
+                                   int32_t* err_flag, void* stream, int64_t entity_begin, int64_t entity_end,
+                                   int32_t csr_ready, int32_t reg_relations) {
+  if (entity_begin < 0 || entity_end < entity_begin || entity_end > (m ? m->nentity : 0)) return KGE_ERR_ARG;
+  return train_impl(m, mode, pos, neg, batch, nneg, subsampling_weight, weight_sum, uni_weight, uni_batch, 1, 1.f,
+                    regularization, adam, grad_entity, grad_relation, grad_modulus, losses_out, workspace,
+                    workspace_bytes, err_flag, stream, KGE_PHASE_ALL, entity_begin, entity_end,
+                    csr_ready ? XS_FROM_ROWS_CSR : XS_FROM_ROWS, const_cast<float*>(g_in), const_cast<float*>(dq_in),
+                    stats_inout, reg_relations ? 1 : 0);
 }
 
 int kge_train_csr(const kge_model_desc* m, int32_t mode, const int64_t* pos, const int64_t* neg, int64_t batch,

@@ -27,8 +27,8 @@ struct FinArgs {
   int64_t B;
   int uni_weight;
   float uni_n;               // global batch size (uni_weight means)
-  const float* reg_partial;  // [nreg] or null
-  int64_t nreg;
+  const float* reg_partial;  // or null; summed over [reg_a0, reg_a1) then [reg_b0, reg_b1)
+  int64_t reg_a0, reg_a1, reg_b0, reg_b1;  // (entity parts, relation rows; a sub-range for an owner's step)
   float regularization;
   float* losses;             // [4]
   float* grad_modulus;       // nullable

@@ -113,9 +113,10 @@ __global__ __launch_bounds__(1024) void k_finalize(FinArgs a) {
 #pragma unroll
   for (int u = 0; u < 6; ++u) tot[u] = red[u][0];
   float reg = 0.f;
-  if (a.reg_partial && a.nreg > 0) {
+  const int64_t na = a.reg_a1 - a.reg_a0, nreg = na + (a.reg_b1 - a.reg_b0);
+  if (a.reg_partial && nreg > 0) {
     float s = 0.f;
-    for (int64_t k = tid; k < a.nreg; k += 1024) s += a.reg_partial[k];
+    for (int64_t v = tid; v < nreg; v += 1024) s += a.reg_partial[v < na ? a.reg_a0 + v : a.reg_b0 + (v - na)];
     __syncthreads();
     red[0][tid] = s;
     __syncthreads();

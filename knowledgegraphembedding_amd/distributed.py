@@ -33,6 +33,13 @@ Two exchanges implement step 3 (`dp_exchange_mode`):
   that is ~13× fewer bytes than the all-reduce, paid for with N× the
   occurrence work of the entity pass; the result is bit-identical to one
   process training on the whole batch.  "auto" picks it for N <= 2.
+* "owner" — the factors as above, but each rank runs the entity-major pass
+  (gradient + fused Adam) only for the 1/N of the entity rows it owns, over
+  the global batch's occurrences, and the updated rows are all-gathered
+  (partition.EntityRowPartition, exchange "factors"): per rank ≈ 9 MB·(N−1) of
+  factors plus (N−1)/N of the table inbound, the occurrence work of one
+  single-GPU entity pass and 1/N of the Adam stream.  "auto" picks it above
+  2 ranks.
 """
 from __future__ import annotations
 
@@ -87,14 +94,17 @@ def dp_allreduce_packed_async(tensors, group=None):
 
 
 def dp_exchange_mode(world: int, override: str | None = None) -> str:
-    """"grads" (overlapped all-reduce of the dense gradient) or "factors"
-    (all-gather of the per-row factors, global entity pass on every rank);
-    KGE_DP_EXCHANGE=auto|grads|factors, auto = factors for up to 2 ranks."""
+    """"grads" (overlapped all-reduce of the dense gradient), "factors"
+    (all-gather of the per-row factors, global entity pass on every rank) or
+    "owner" (the factors all-gathered, each rank's entity pass and Adam on the
+    1/N of the rows it owns, the updated rows all-gathered: partition.py);
+    KGE_DP_EXCHANGE=auto|grads|factors|owner, auto = factors for up to 2
+    ranks, owner above (DESIGN.md §9 byte model)."""
     mode = override or os.environ.get("KGE_DP_EXCHANGE", "auto")
     if mode == "auto":
-        return "factors" if world <= 2 else "grads"
-    if mode not in ("grads", "factors"):
-        raise ValueError(f"KGE_DP_EXCHANGE must be auto, grads or factors, not {mode!r}")
+        return "factors" if world <= 2 else "owner"
+    if mode not in ("grads", "factors", "owner"):
+        raise ValueError(f"KGE_DP_EXCHANGE must be auto, grads, factors or owner, not {mode!r}")
     return mode
 
 
@@ -131,15 +141,18 @@ def fx_pieces(B: int, chunks: int = FX_CHUNKS):
     return [(c * step, (c + 1) * step) for c in range(k)]
 
 
-def dp_train_step_factors(model, positive_sample, negative_sample, subsampling_weight, mode, args,
-                          optimizer=None):
-    """One data-parallel step by factor exchange (module docstring): Σw over the
-    gathered weights, the row pass on this rank's rows into its place in the
-    gather buffers (in FX_CHUNKS pieces, each piece's all-gather overlapping the
-    next piece's row pass), an all-gather of those buffers, then the rest of the step
-    for the global batch on every rank (the fused Adam update included when the
-    optimizer is a KGEAdam).  Returns the global [5] loss vector (the same on
-    every rank, nothing left to reduce)."""
+class RowFactors:
+    """The gathered inputs of the global step (see _exchange_row_factors)."""
+    __slots__ = ("pos", "neg", "w", "wsum", "g", "dq", "stats", "workspace", "B", "uni")
+
+
+def _exchange_row_factors(model, positive_sample, negative_sample, subsampling_weight, mode, args) -> RowFactors:
+    """Everything the factor-exchanging steps share: the global batch's ids and
+    weights all-gathered, Σw over them, this rank's row pass into its place in
+    the gather buffers (in FX_CHUNKS pieces, each piece's all-gather overlapping
+    the next piece's row pass), the gathered dL/ds, dL/dq and row statistics,
+    and the global batch's occurrence CSR built on a side stream as soon as the
+    ids arrive (FX_CSR_AHEAD, into `workspace`)."""
     from . import ops
     group = args.dp_group
     world = dist.get_world_size(group)
@@ -216,15 +229,31 @@ def dp_train_step_factors(model, positive_sample, negative_sample, subsampling_w
         h.wait()
     if side is not None:
         torch.cuda.current_stream(dev).wait_stream(side)
+    fx = RowFactors()
+    fx.pos, fx.neg, fx.w, fx.wsum, fx.g, fx.dq, fx.stats, fx.workspace, fx.B, fx.uni = (
+        pos_g, neg_g, w_g, wsum, g_g, dq_g, st_g, gws, Bg, uni)
+    return fx
+
+
+def dp_train_step_factors(model, positive_sample, negative_sample, subsampling_weight, mode, args,
+                          optimizer=None):
+    """One data-parallel step by factor exchange (module docstring): the row
+    factors exchanged (_exchange_row_factors), then the rest of the step for
+    the global batch on every rank (the fused Adam update included when the
+    optimizer is a KGEAdam).  Returns the global [5] loss vector (the same on
+    every rank, nothing left to reduce)."""
+    from . import ops
+    dev = model.entity_embedding.device
+    fx = _exchange_row_factors(model, positive_sample, negative_sample, subsampling_weight, mode, args)
     adam = None
     if optimizer is not None and model.fuse_optimizer and hasattr(optimizer, 'prepare_fused'):
         adam = optimizer.prepare_fused(model.entity_embedding, model.relation_embedding, model._modulus(),
                                        write_grad=model.keep_grads)
     ge, gr, gm, losses = model._grad_buffers()
-    ops.train_step_from_rows(desc, mode, pos_g, neg_g, w_g, wsum, dev, uni_weight=uni, uni_batch=Bg,
-                             regularization=float(args.regularization), g_in=g_g, dq_in=dq_g, stats=st_g,
-                             grad_entity=ge, grad_relation=gr, grad_modulus=gm, losses=losses, adam=adam,
-                             csr_ready=FX_CSR_AHEAD, workspace=gws)
+    ops.train_step_from_rows(model.desc(), mode, fx.pos, fx.neg, fx.w, fx.wsum, dev, uni_weight=fx.uni,
+                             uni_batch=fx.B, regularization=float(args.regularization), g_in=fx.g, dq_in=fx.dq,
+                             stats=fx.stats, grad_entity=ge, grad_relation=gr, grad_modulus=gm, losses=losses,
+                             adam=adam, csr_ready=FX_CSR_AHEAD, workspace=fx.workspace)
     if model.entity_embedding.requires_grad:
         model.entity_embedding.grad = ge
     if model.relation_embedding.requires_grad:

@@ -383,7 +383,8 @@ class KGEModel(nn.Module):
         dp = getattr(args, 'dp_group', None)
         if part is not None:
             # row-partitioned entity table (partition.py): reduce-scatter to the owners
-            losses = part.train_grads(model, positive_sample, negative_sample, subsampling_weight, mode, args)
+            losses = part.train_grads(model, positive_sample, negative_sample, subsampling_weight, mode, args,
+                                      optimizer=optimizer)
         elif dp is not None:
             import torch.distributed as dist
             from .distributed import dp_exchange_mode, dp_train_grads, dp_train_step_factors

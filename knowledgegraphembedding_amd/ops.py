@@ -301,11 +301,14 @@ def train_step_from_rows(desc: _lib.ModelDesc, mode: str, pos: torch.Tensor, neg
                          regularization: float, g_in: torch.Tensor, dq_in: torch.Tensor, stats: torch.Tensor,
                          grad_entity: torch.Tensor, grad_relation: torch.Tensor, grad_modulus: Optional[torch.Tensor],
                          losses: torch.Tensor, adam: Optional[_lib.AdamDesc] = None, csr_ready: bool = False,
-                         workspace: Optional[torch.Tensor] = None) -> None:
+                         workspace: Optional[torch.Tensor] = None, entity_range: Optional[tuple] = None,
+                         reg_relations: bool = True) -> None:
     """The rest of the step for the whole (gathered) batch from the exchanged
     row factors (kge_train_step_from_rows; with csr_ready the CSR train_csr
     built for this batch, kge_train_step_from_rows_csr); bit-identical to one
-    process running train_step_grads / the fused step on that batch."""
+    process running train_step_grads / the fused step on that batch.  With
+    `entity_range` (e0, e1) the entity-major pass and its Adam cover only those
+    rows (the owner-computes step, kge_train_step_from_rows_range)."""
     if mode not in ("head-batch", "tail-batch"):
         raise ValueError("Training batch mode %s not supported" % mode)
     pos, neg = _idx(pos, dev), _idx(neg, dev)
@@ -314,12 +317,18 @@ def train_step_from_rows(desc: _lib.ModelDesc, mode: str, pos: torch.Tensor, neg
     _check_row_buffers(dev, B, n, desc.entity_dim, g_in, dq_in, stats)
     ws = workspace if workspace is not None else _train_ws(desc, B, n, dev)
     st = state(dev)
+    args = (desc, _lib.MODE_IDS[mode], pos.data_ptr(), neg.data_ptr(), B, n, w.data_ptr(), _ptr(weight_sum_dev),
+            int(bool(uni_weight)), int(uni_batch), float(regularization), g_in.data_ptr(), dq_in.data_ptr(),
+            stats.data_ptr(), adam, grad_entity.data_ptr(), grad_relation.data_ptr(), _ptr(grad_modulus),
+            losses.data_ptr(), ws.data_ptr(), ws.numel(), st.err.data_ptr(), _stream(dev))
+    if entity_range is not None:
+        e0, e1 = entity_range
+        _lib.check(_lib.load().kge_train_step_from_rows_range(*args, int(e0), int(e1), int(bool(csr_ready)),
+                                                              int(bool(reg_relations))),
+                   "kge_train_step_from_rows_range")
+        return
     fn = "kge_train_step_from_rows_csr" if csr_ready else "kge_train_step_from_rows"
-    _lib.check(getattr(_lib.load(), fn)(
-        desc, _lib.MODE_IDS[mode], pos.data_ptr(), neg.data_ptr(), B, n, w.data_ptr(), _ptr(weight_sum_dev),
-        int(bool(uni_weight)), int(uni_batch), float(regularization), g_in.data_ptr(), dq_in.data_ptr(),
-        stats.data_ptr(), adam, grad_entity.data_ptr(), grad_relation.data_ptr(), _ptr(grad_modulus),
-        losses.data_ptr(), ws.data_ptr(), ws.numel(), st.err.data_ptr(), _stream(dev)), fn)
+    _lib.check(getattr(_lib.load(), fn)(*args), fn)
 
 
 def adam_step(param: torch.Tensor, grad: torch.Tensor, exp_avg: torch.Tensor, exp_avg_sq: torch.Tensor, *,

@@ -72,6 +72,26 @@ class KGEAdam(torch.optim.Optimizer):
             self._fused_done.add(id(p))
         return desc
 
+    def prepare_fused_rows(self, shard, table, row0, relation, modulus=None, write_grad=True):
+        """prepare_fused for an owner of entity rows [row0, row0 + len(shard)):
+        `shard` is the optimizer's parameter (a view of those rows of `table`,
+        whose moments are shard-sized); the descriptor points the entity
+        update at `table` and its moments `row0` rows before the shard's, so
+        the kernels index them by global row (kge_train_step_from_rows_range
+        touches only the owned rows).  None if the configuration does not fit."""
+        from . import _lib
+        if shard.data_ptr() != table.data_ptr() + row0 * table.stride(0) * table.element_size():
+            return None
+        desc = self.prepare_fused(shard, relation, modulus, write_grad)
+        if desc is None:
+            return None
+        off = row0 * table.stride(0) * table.element_size()
+        st = self.state[shard]
+        desc.entity.param = table.data_ptr()
+        desc.entity.exp_avg = st['exp_avg'].data_ptr() - off
+        desc.entity.exp_avg_sq = st['exp_avg_sq'].data_ptr() - off
+        return desc
+
     @torch.no_grad()
     def step_param(self, p, chunks=None, before_chunk=None) -> bool:
         """Apply this step's update to ONE parameter now — row range by row

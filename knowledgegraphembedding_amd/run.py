@@ -246,13 +246,23 @@ def main(args):
         for p in kge_model.parameters():
             dist.broadcast(p.data, src=0)
     part = None
-    if getattr(args, 'row_partition', False):
-        if args.dp_group is None:
-            logging.info('--row_partition ignored: one process (launch with torchrun for a partitioned table)')
-        else:
-            from .partition import EntityRowPartition
-            part = EntityRowPartition(kge_model, args.dp_group)
-            logging.info('Entity rows partitioned: rank %d owns [%d, %d)' % (rank, part.lo, part.hi))
+    owner = False
+    if args.dp_group is not None:
+        from .distributed import dp_exchange_mode
+        owner = dp_exchange_mode(torch.distributed.get_world_size(args.dp_group),
+                                 getattr(args, 'dp_exchange', None)) == "owner"
+    if getattr(args, 'row_partition', False) and args.dp_group is None:
+        logging.info('--row_partition ignored: one process (launch with torchrun for a partitioned table)')
+    elif getattr(args, 'row_partition', False) or owner:
+        # --row_partition: exchange KGE_PART_EXCHANGE ("factors": owner-computes
+        # from the exchanged row factors; "grads": reduce-scatter of the dense
+        # gradient); the data-parallel "owner" exchange is the former
+        from .partition import EntityRowPartition
+        exchange = os.environ.get('KGE_PART_EXCHANGE', 'factors') if getattr(args, 'row_partition', False) \
+            else 'factors'
+        part = EntityRowPartition(kge_model, args.dp_group, exchange=exchange)
+        logging.info('Entity rows partitioned (%s exchange): rank %d owns [%d, %d)' % (exchange, rank, part.lo,
+                                                                                        part.hi))
 
     def trainable():
         return part.parameters() if part is not None else filter(lambda p: p.requires_grad, kge_model.parameters())

@@ -184,7 +184,7 @@ def test_factor_exchange_gathers_global_batch(uni, world):
     dq = torch.empty(B, LE)
     st = torch.empty(B, 4)
     _fx_rows(pos, neg, w, g, dq, st)  # the stand-in over the whole batch = the two slices concatenated
-    assert kdist.dp_exchange_mode(2) == "factors" and kdist.dp_exchange_mode(8) == "grads"
+    assert kdist.dp_exchange_mode(2) == "factors" and kdist.dp_exchange_mode(8) == "owner"
     for rank in range(world):
         s = out[rank]["seen"]
         for got, want in zip(s["global"], (pos, neg, w, g, dq, st)):
