@@ -76,7 +76,7 @@ def _worker(rank, world, port, name, reg, uni, out):
 
 @pytest.mark.parametrize("name,reg,uni,world", [("RotatE", 0.0, False, 2), ("RotatE", 0.0, False, 4),
                                                 ("ComplEx", 1e-4, False, 4), ("pRotatE", 0.0, True, 2),
-                                                ("TransE", 0.0, False, 3), ("DistMult", 1e-4, True, 2)])
+                                                ("TransE", 0.0, False, 4), ("DistMult", 1e-4, True, 2)])
 def test_owner_exchange_bitwise(name, reg, uni, world):
     out = mp.Manager().dict()
     mp.spawn(_worker, args=(world, _free_port(), name, reg, uni, out), nprocs=world, join=True)
