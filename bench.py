@@ -215,6 +215,48 @@ def cpu_baseline(model_cpu_state, budget_s: float = 12.0, b: int = 32):
                       f"torch threads = {cores}"}
 
 
+def rank_section(dev, reps: int = 3) -> dict:
+    """BASELINE config 3, measured live beside the training metric: filtered
+    ranking (KGEModel.rank_queries → kge_rank_filtered: MFMA tile + near-tie
+    refinement in the reference's order) of all 3134 wn18rr-shape test triples
+    in both directions (6268 queries, E=40943, d=500) against a synthetic
+    filter graph of wn18rr's 93,003 true triples (tools/bench_rank.py, same
+    data).  `tflops` = 2·queries·E·K / wall time of the whole pass (host CSR,
+    bitmap, window, MFMA tile, refinement, read-back): a lower bound on the
+    MFMA tile's own rate (its rocprofv3 time: profiles/r02/rank_*)."""
+    import numpy as np
+    from knowledgegraphembedding_amd import synth
+    from knowledgegraphembedding_amd.filters import FilterIndex
+    Ew, Rw, ntrue, ntest, d = 40943, 11, 93003, 3134, 500
+    h, r, t = synth.randint(901, (ntrue,), Ew), synth.randint(902, (ntrue,), Rw), synth.randint(903, (ntrue,), Ew)
+    true = np.unique(np.stack([h, r, t], 1), axis=0)
+    test = true[synth.randint(904, (ntest,), len(true))]
+    index = FilterIndex(true, Ew, Rw)
+    out = {"workload": "wn18rr-shape filtered ranking (config 3), synthetic graph, both directions",
+           "queries": 2 * ntest, "entities": Ew, "hidden_dim": d}
+    for name, cplx in (("DistMult", False), ("ComplEx", True)):
+        torch.manual_seed(0)
+        m = KGEModel(name, Ew, Rw, d, 12.0, cplx, cplx).to(dev)
+        K = m.entity_dim
+        best = None
+        for rep in range(reps + 1):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            rh, _ = m.rank_queries(test, index, "head-batch")
+            rt, _ = m.rank_queries(test, index, "tail-batch")
+            torch.cuda.synchronize()
+            dt = time.perf_counter() - t0
+            if rep and (best is None or dt < best):
+                best = dt
+        flops = 2.0 * 2 * ntest * Ew * K
+        out[name] = {"ms": best * 1e3, "queries_per_s": 2 * ntest / best, "tflops": flops / best / 1e12,
+                     "fp32_mfma_peak_tflops": 157.3, "frac": flops / best / 1e12 / 157.3,
+                     "mrr": float(np.mean(1.0 / np.concatenate([rh, rt])))}
+        del m
+    torch.cuda.empty_cache()
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -225,6 +267,7 @@ def main():
     ap.add_argument("--no-stage-timer", action="store_true",
                     help="skip the per-stage HIP events (roofline then comes from the committed rocprof summary)")
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="fb15k")
+    ap.add_argument("--no-rank", action="store_true", help="skip the config-3 ranking section (rank 0, 1 GPU)")
     ap.add_argument("--traffic-json", default=None,
                     help="rocprofv3 PMC summary (tools/pmc_traffic.py output) for roofline.traffic "
                          "(default: the committed profiles/pmc_traffic.json of this workload)")
@@ -374,6 +417,8 @@ def main():
                       out["step_roofline"].get("frac_traffic")) if x is not None]
     if any(f > 1.0 for f in fr):
         print(f"bench.py: a roofline fraction exceeds 1 ({fr}); the byte model is wrong", file=sys.stderr)
+    if rank == 0 and world == 1 and not a.no_rank and a.workload == "fb15k":
+        out["ranking"] = rank_section(dev)
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(cpu_state, budget_s=a.cpu_budget)
     if rank == 0:

@@ -292,32 +292,53 @@ int launch_rank_mfma(int gather, const float* q, const float* ent, int64_t nq, i
 
 // Entity-table statistics for the ranking windows: stats[0] = max row L2
 // norm, stats[1] = max |x| (non-negative floats order like their bit
-// patterns, so an integer atomicMax is exact).  One wave per row.
+// patterns, so an integer atomicMax is exact).  One wave per row, rows
+// strided over a bounded grid; the block's four waves combine in LDS and the
+// block issues one atomic per statistic (an atomic per row on the same two
+// words serialised: 0.93 ms for wn18rr's 40,943 rows).
 __global__ __launch_bounds__(256) void k_table_stats(const float* __restrict__ ent, int64_t E, int Le,
                                                      float* stats) {
-  const int lane = threadIdx.x & 63;
-  const int64_t e = (int64_t)blockIdx.x * 4 + wave_id();
-  if (e >= E) return;
-  const float* row = ent + e * Le;
-  float s2 = 0.f, mx = 0.f;
-  for (int k = lane; k < Le; k += 64) {
-    const float v = row[k];
-    s2 += v * v;
-    mx = fmaxf(mx, fabsf(v));
-  }
-  s2 = wave_sum(s2);
+  __shared__ float red[2][4];
+  const int lane = threadIdx.x & 63, w = wave_id();
+  float bn = 0.f, bm = 0.f;
+  for (int64_t e = (int64_t)blockIdx.x * 4 + w; e < E; e += (int64_t)gridDim.x * 4) {
+    const float* row = ent + e * Le;
+    float s2 = 0.f, mx = 0.f;
+    if ((Le & 3) == 0 && (((uintptr_t)ent) & 15) == 0) {  // float4 rows
+      for (int k = lane; k < Le / 4; k += 64) {
+        const float4 v = reinterpret_cast<const float4*>(row)[k];
+        s2 += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+        mx = fmaxf(mx, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+      }
+    } else {
+      for (int k = lane; k < Le; k += 64) {
+        const float v = row[k];
+        s2 += v * v;
+        mx = fmaxf(mx, fabsf(v));
+      }
+    }
+    s2 = wave_sum(s2);
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
-  if (lane == 0) {
-    atomicMax(reinterpret_cast<unsigned int*>(&stats[0]), __float_as_uint(sqrtf(s2) * 1.0001f));
-    atomicMax(reinterpret_cast<unsigned int*>(&stats[1]), __float_as_uint(mx));
+    for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+    bn = fmaxf(bn, sqrtf(s2) * 1.0001f);
+    bm = fmaxf(bm, mx);
+  }
+  if (lane == 0) { red[0][w] = bn; red[1][w] = bm; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const float n = fmaxf(fmaxf(red[0][0], red[0][1]), fmaxf(red[0][2], red[0][3]));
+    const float m = fmaxf(fmaxf(red[1][0], red[1][1]), fmaxf(red[1][2], red[1][3]));
+    atomicMax(reinterpret_cast<unsigned int*>(&stats[0]), __float_as_uint(n));
+    atomicMax(reinterpret_cast<unsigned int*>(&stats[1]), __float_as_uint(m));
   }
 }
 
 int launch_table_stats(const float* ent, int64_t E, int Le, float* stats, hipStream_t s) {
   hipError_t e = hipMemsetAsync(stats, 0, 2 * sizeof(float), s);
   if (e != hipSuccess) return (int)e;
-  hipLaunchKernelGGL(k_table_stats, dim3((unsigned)((E + 3) / 4)), dim3(256), 0, s, ent, E, Le, stats);
+  const int64_t blocks = (E + 3) / 4;
+  hipLaunchKernelGGL(k_table_stats, dim3((unsigned)(blocks < 2048 ? blocks : 2048)), dim3(256), 0, s, ent, E, Le,
+                     stats);
   return (int)hipGetLastError();
 }
 

@@ -7,7 +7,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 STEPS=${STEPS:-200}
 for v in "$@"; do
-  env $v timeout -k 10 ${BENCH_TIMEOUT:-300} python bench.py --steps $STEPS --warmup 5 --no-cpu-baseline ${BENCH_ARGS:-} > gpurun_out/ab_one.json 2> gpurun_out/ab_one.err
+  env $v timeout -k 10 ${BENCH_TIMEOUT:-300} python bench.py --steps $STEPS --warmup 5 --no-cpu-baseline --no-rank ${BENCH_ARGS:-} > gpurun_out/ab_one.json 2> gpurun_out/ab_one.err
   rc=$?
   if [ $rc -ne 0 ]; then echo "variant '$v' rc=$rc"; tail -20 gpurun_out/ab_one.err; exit $rc; fi
   python - "$v" <<'PY'

@@ -8,7 +8,7 @@ mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
 for kv in ${ENVS:-}; do export "$kv"; done
 timeout -k 10 300 rocprofv3 --pmc $COUNTERS --kernel-trace --output-format csv -d "$OUT" -o run -- \
-  python3 "$ROOT/bench.py" --steps 12 --warmup 2 --no-cpu-baseline --no-stage-timer > "$OUT/bench.json" 2> "$OUT/err.log"
+  python3 "$ROOT/bench.py" --steps 12 --warmup 2 --no-cpu-baseline --no-rank --no-stage-timer > "$OUT/bench.json" 2> "$OUT/err.log"
 rc=$?; [ $rc -ne 0 ] && { tail -20 "$OUT/err.log"; exit $rc; }
 python3 - "$OUT" <<'PY'
 import csv, glob, sys, collections

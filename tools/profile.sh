@@ -7,7 +7,7 @@ OUT="$ROOT/gpurun_out/prof"
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
 STEPS=${STEPS:-20}
-BARGS="$ROOT/bench.py --steps $STEPS --warmup 3 --no-cpu-baseline"
+BARGS="$ROOT/bench.py --steps $STEPS --warmup 3 --no-cpu-baseline --no-rank"
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- python3 $BARGS > "$OUT/bench_trace.json" 2> "$OUT/trace.err"
 rc=$?; echo "trace rc=$rc"; [ $rc -ne 0 ] && { tail -20 "$OUT/trace.err"; exit $rc; }
 if [ "${PMC:-1}" = "1" ]; then
