@@ -336,8 +336,8 @@ __global__ __launch_bounds__(256) void k_table_stats(const float* __restrict__ e
 int launch_table_stats(const float* ent, int64_t E, int Le, float* stats, hipStream_t s) {
   hipError_t e = hipMemsetAsync(stats, 0, 2 * sizeof(float), s);
   if (e != hipSuccess) return (int)e;
-  const int64_t blocks = (E + 3) / 4;
-  hipLaunchKernelGGL(k_table_stats, dim3((unsigned)(blocks < 2048 ? blocks : 2048)), dim3(256), 0, s, ent, E, Le,
+  const int64_t blocks = (E + 3) / 4;  // one row per wave: every row in flight at once
+  hipLaunchKernelGGL(k_table_stats, dim3((unsigned)(blocks < 65535 ? blocks : 65535)), dim3(256), 0, s, ent, E, Le,
                      stats);
   return (int)hipGetLastError();
 }
