@@ -36,6 +36,27 @@ class FilterIndex:
             o = np.lexsort((t[:, 0], k_rt))
             self._k_rt, self._heads = k_rt[o], t[o, 0]
 
+    # query keys (h·R + r or r·E + t) span E·R values: up to this many, the
+    # [lo, hi) range of every key is tabulated once (two int32 arrays per mode)
+    # and a lookup is one gather; above, binary searches of the sorted keys
+    DENSE_KEYS = 1 << 22
+
+    def _range(self, cand, keys, tag):
+        if self.nentity * self.nrelation <= self.DENSE_KEYS:
+            tab = getattr(self, tag, None)
+            if tab is None:
+                n = self.nentity * self.nrelation
+                start = np.searchsorted(cand, np.arange(n + 1, dtype=np.int64), side='left').astype(np.int32)
+                tab = start
+                setattr(self, tag, tab)
+            return tab[keys].astype(np.int64), tab[keys + 1].astype(np.int64)
+        o = np.argsort(keys, kind='stable')  # sorted probes: the searches walk the array forward
+        ks = keys[o]
+        lo, hi = np.empty_like(keys), np.empty_like(keys)
+        lo[o] = np.searchsorted(cand, ks, side='left')
+        hi[o] = np.searchsorted(cand, ks, side='right')
+        return lo, hi
+
     def filter_csr(self, queries, mode: str):
         """(offsets [nq+1] int64, ids int64) of the filtered candidates per query."""
         q = np.asarray(queries, dtype=np.int64).reshape(-1, 3)
@@ -47,8 +68,7 @@ class FilterIndex:
             true = q[:, 0]
         else:
             raise ValueError('negative batch mode %s not supported' % mode)
-        lo = np.searchsorted(cand, keys, side='left')
-        hi = np.searchsorted(cand, keys, side='right')
+        lo, hi = self._range(cand, keys, '_tab_hr' if mode == 'tail-batch' else '_tab_rt')
         cnt = hi - lo
         total = int(cnt.sum())
         if total == 0:
