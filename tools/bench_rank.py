@@ -6,8 +6,8 @@ wn18rr shape (E=40943, R=11) d=500, all 3134 test triples × both directions
 Synthetic graph: 93,003 true triples (wn18rr's train+valid+test count) drawn
 uniformly; tables U(-range, range).  Reports queries/s, the launch time, and
 the MFMA roofline (2·nq·E·K flops ÷ time vs 157.3 TF fp32 dense).
-Set KGE_RANK_MFMA=0 to time the register-tiled VALU kernel instead, and
-KGE_RANK_TILE=0 as well for the per-pair wave-reduction scan.
+--path tile times the register-tiled VALU kernel instead of the MFMA tile for
+DistMult/ComplEx, --path scan the per-pair wave-reduction scan.
 
     python tools/bench_rank.py [--models DistMult ComplEx RotatE] [--reps 3] [--cpu-sample 8]
 """
@@ -31,12 +31,13 @@ DIMS = {"DistMult": (False, False), "ComplEx": (True, True), "RotatE": (True, Fa
         "pRotatE": (False, False)}
 
 
-def rank_path(name, K):
-    """Which kernel kge_rank_filtered picks (kge_capi.hip: use_mfma_rank / use_tile_rank)."""
+def rank_path(name, K, path="auto"):
+    """Which fast pass kge_rank_filtered_ex runs (kge_capi.hip rank_path)."""
     red = K // 2 if name in ("RotatE", "ComplEx") else K
-    if name in ("DistMult", "ComplEx") and os.environ.get("KGE_RANK_MFMA", "1") != "0" and K % 4 == 0:
+    mfma_ok = name in ("DistMult", "ComplEx") and K % 4 == 0
+    if path == "mfma" or (path == "auto" and mfma_ok):
         return "mfma"
-    if os.environ.get("KGE_RANK_TILE", "1") != "0" and red % 4 == 0:
+    if path in ("auto", "tile") and red % 4 == 0:
         return "valu-tile"
     return "valu-scan"
 
@@ -46,6 +47,7 @@ def main():
     ap.add_argument("--models", nargs="+", default=["DistMult", "ComplEx"])
     ap.add_argument("-d", "--hidden_dim", type=int, default=500)
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--path", default="auto", choices=("auto", "mfma", "tile", "scan"))
     ap.add_argument("--cpu-sample", type=int, default=0, help="queries timed through the CPU oracle (0: skip)")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
@@ -66,8 +68,8 @@ def main():
         for rep in range(a.reps + 1):
             torch.cuda.synchronize()
             t0 = time.perf_counter()
-            rh, _ = m.rank_queries(test, index, "head-batch")
-            rt, _ = m.rank_queries(test, index, "tail-batch")
+            rh, _ = m.rank_queries(test, index, "head-batch", path=a.path)
+            rt, _ = m.rank_queries(test, index, "tail-batch", path=a.path)
             torch.cuda.synchronize()
             if rep:
                 times.append(time.perf_counter() - t0)
@@ -78,7 +80,7 @@ def main():
         res = {"model": name, "hidden_dim": a.hidden_dim, "entity_dim": K, "queries": nq,
                "seconds": dt, "queries_per_s": nq / dt, "candidate_scores_per_s": nq * E / dt,
                "tflops": flops / dt / 1e12,
-               "path": rank_path(name, K),
+               "path": rank_path(name, K, a.path),
                "pair_terms_per_s": nq * E * (K // 2 if name in ("RotatE", "ComplEx") else K) / dt,
                "mrr": float(np.mean(1.0 / ranks))}
         if res["path"] == "mfma":

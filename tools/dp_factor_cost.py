@@ -1,8 +1,10 @@
 #!/usr/bin/env python3
 """Compute side of the data-parallel factor exchange on one GPU (RotatE FB15k
-shape): the per-rank row pass on 1024 rows (kge_train_rows_slice) and the
+shape): the per-rank row pass on 1024 rows (kge_train_rows_slice), the
 global step (kge_train_step_from_rows, fused Adam) on N·1024 gathered rows,
-for N = 1, 2, 4, 8 — against the single-device fused step.  Prints one JSON
+and the owner-computes step (the same, entity pass + Adam on the 1/N of the
+rows one rank owns, kge_train_step_from_rows_range), for N = 1, 2, 4, 8 —
+against the single-device fused step.  Prints one JSON
 line; the exchange itself moves (B·Le + B·n + 4B)·4 + B·(n+3)·8 bytes per rank.
 
     python tools/dp_factor_cost.py [--reps 30]
@@ -91,6 +93,23 @@ def main():
             opt.step()
         ops.train_csr(desc, "tail-batch", pg, ng, dev)
         res[f"global_step_ms_N{world}_csr_ahead"] = timed(glob_csr, a.reps)
+
+        # the "owner" exchange: the same global step, but the entity pass and
+        # its fused Adam only over the 1/N of the rows rank 0 owns
+        rows_own = -(-E // world)
+        shard = torch.nn.Parameter(m.entity_embedding.data[:rows_own])
+        oopt = KGEAdam([shard, m.relation_embedding], lr=1e-4)
+
+        def owner():
+            adam = oopt.prepare_fused_rows(shard, m.entity_embedding, 0, m.relation_embedding, None, write_grad=True)
+            ops.train_step_from_rows(desc, "tail-batch", pg, ng, wg, wsum, dev, uni_weight=False, uni_batch=Bg,
+                                     regularization=0.0, g_in=g_g, dq_in=dq_g, stats=st_g, grad_entity=ge,
+                                     grad_relation=gr, grad_modulus=gm, losses=losses, adam=adam, csr_ready=True,
+                                     entity_range=(0, rows_own), reg_relations=True)
+            oopt.step()
+        ops.train_csr(desc, "tail-batch", pg, ng, dev)
+        res[f"owner_step_ms_N{world}_csr_ahead"] = timed(owner, a.reps)
+        res[f"owner_rows_allgather_bytes_in_N{world}"] = (world - 1) * rows_own * Le * 4
         res[f"csr_ms_N{world}"] = timed(lambda: ops.train_csr(desc, "tail-batch", pg, ng, dev), a.reps)
         res[f"exchange_bytes_per_rank_N{world}"] = (B * Le + B * N + 4 * B) * 4 + B * (N + 3) * 8 + 4 * B
     res["allreduce_bytes_per_rank_grads"] = {f"N{k}": 2 * (k - 1) / k * E * Le * 4 for k in (2, 4, 8)}
