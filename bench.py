@@ -357,12 +357,21 @@ def main():
     here = os.path.dirname(os.path.abspath(__file__))
     row_ms = float(stage[1]) / calls
     ent_ms = float(stage[4]) / calls
-    row_bytes = algorithmic_row_bytes(B, NNEG, 2 * D, D)
+    # the factor / owner exchanges run the row pass in pieces (each timed call
+    # is one piece) and the entity pass outside the timed call: the entity and
+    # whole-step rooflines are single-process figures only
+    exchanged = group is not None and (part is not None or dp_mode in ("factors", "owner"))
+    row_rows = B
+    if exchanged:
+        from knowledgegraphembedding_amd.distributed import fx_pieces
+        row_rows = fx_pieces(B)[0][1]
+        ent_ms = 0.0
+    row_bytes = algorithmic_row_bytes(row_rows, NNEG, 2 * D, D)
     ent_bytes = algorithmic_entity_bytes(E, R, B, NNEG, 2 * D, D)
     achieved = row_bytes / (row_ms * 1e-3) / 1e9 if row_ms > 0 else None
     ent_achieved = ent_bytes / (ent_ms * 1e-3) / 1e9 if ent_ms > 0 else None
     row_traffic = ent_traffic = None
-    if a.workload == "fb15k":  # PMC summaries of this workload (tools/profile.sh + tools/pmc_traffic.py)
+    if a.workload == "fb15k" and not exchanged:  # PMC summaries of this workload (tools/profile.sh + tools/pmc_traffic.py)
         row_traffic = _pmc_bytes(a.traffic_json or os.path.join(here, "profiles", "pmc_traffic.json"))
         ent_traffic = _pmc_bytes(os.path.join(here, "profiles", "pmc_traffic_entity.json"))
 
@@ -409,12 +418,18 @@ def main():
                             "achieved": ent_achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                             "frac": ent_achieved / HBM_PEAK_GBS if ent_achieved else None, "traffic": ent_traffic,
                             "algorithmic_bytes_per_launch": ent_bytes, "avg_launch_ms": ent_ms},
-        "step_roofline": step_roofline(dt / a.steps, row_bytes, ent_bytes, row_traffic, ent_traffic),
+        "step_roofline": None if exchanged else step_roofline(dt / a.steps, row_bytes, ent_bytes, row_traffic,
+                                                                 ent_traffic),
     }
+    if exchanged:
+        out["roofline"]["rows_per_launch"] = row_rows
+        out["roofline_entity"] = None
     if a.workload != "fb15k":
         out["metric"] = f"scored (pos+neg) triples/sec, RotatE {a.workload} d={D} b={B} n={NNEG}"
-    fr = [x for x in (out["roofline"]["frac"], out["roofline_entity"]["frac"], out["step_roofline"]["frac"],
-                      out["step_roofline"].get("frac_traffic")) if x is not None]
+    fr = [out["roofline"]["frac"]]
+    if not exchanged:
+        fr += [out["roofline_entity"]["frac"], out["step_roofline"]["frac"], out["step_roofline"].get("frac_traffic")]
+    fr = [x for x in fr if x is not None]
     if any(f > 1.0 for f in fr):
         print(f"bench.py: a roofline fraction exceeds 1 ({fr}); the byte model is wrong", file=sys.stderr)
     if rank == 0 and world == 1 and not a.no_rank and a.workload == "fb15k":

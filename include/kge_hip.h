@@ -268,6 +268,25 @@ int kge_train_step_from_rows_range(const kge_model_desc *m, int32_t mode, const 
                                    int32_t *err_flag, void *stream, int64_t entity_begin, int64_t entity_end,
                                    int32_t csr_ready, int32_t reg_relations);
 
+/*
+ * kge_train_step_from_rows_range in phases (KGE_PHASE_ROWS: q rebuilt, the
+ * positive epilogue, the relation pass; KGE_PHASE_ENTITY: the entity-major
+ * pass + fused Adam of the rows [entity_begin, entity_end); KGE_PHASE_FINALIZE:
+ * the losses, with the regulariser over [entity_begin, entity_end)), the same
+ * arguments in every call.  An owner runs ROWS once, ENTITY once per chunk of
+ * its rows — the all-gather of each finished chunk overlapping the next
+ * chunk's pass — and FINALIZE over its whole range: bit-identical to one
+ * kge_train_step_from_rows_range call.
+ */
+int kge_train_step_from_rows_phased(const kge_model_desc *m, int32_t mode, const int64_t *pos, const int64_t *neg,
+                                    int64_t batch, int64_t nneg, const float *subsampling_weight,
+                                    const float *weight_sum, int32_t uni_weight, int64_t uni_batch,
+                                    float regularization, const float *g_in, const float *dq_in, float *stats_inout,
+                                    const kge_adam_desc *adam, float *grad_entity, float *grad_relation,
+                                    float *grad_modulus, float *losses_out, void *workspace, size_t workspace_bytes,
+                                    int32_t *err_flag, void *stream, int32_t phases, int64_t entity_begin,
+                                    int64_t entity_end, int32_t csr_ready, int32_t reg_relations);
+
 
 /*
  * Σ subsampling_weight into *out (device scalar) — the denominator of

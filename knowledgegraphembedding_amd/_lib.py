@@ -100,6 +100,11 @@ SIGNATURES = {
         [_DESC, _I32, _P, _P, _I64, _I64, _P, _P, _I32, _I64, _F, _P, _P, _P, C.POINTER(AdamDesc), _P, _P, _P, _P,
          _P, _SZ, _P, _P, _I64, _I64, _I32, _I32],
     ),
+    "kge_train_step_from_rows_phased": (
+        C.c_int,
+        [_DESC, _I32, _P, _P, _I64, _I64, _P, _P, _I32, _I64, _F, _P, _P, _P, C.POINTER(AdamDesc), _P, _P, _P, _P,
+         _P, _SZ, _P, _P, _I32, _I64, _I64, _I32, _I32],
+    ),
     "kge_train_step_from_rows_csr": (
         C.c_int,
         [_DESC, _I32, _P, _P, _I64, _I64, _P, _P, _I32, _I64, _F, _P, _P, _P, C.POINTER(AdamDesc), _P, _P, _P, _P,

@@ -613,6 +613,23 @@ int kge_train_step_from_rows_range(const kge_model_desc* m, int32_t mode, const 
                     stats_inout, reg_relations ? 1 : 0);
 }
 
+int kge_train_step_from_rows_phased(const kge_model_desc* m, int32_t mode, const int64_t* pos, const int64_t* neg,
+                                    int64_t batch, int64_t nneg, const float* subsampling_weight,
+                                    const float* weight_sum, int32_t uni_weight, int64_t uni_batch,
+                                    float regularization, const float* g_in, const float* dq_in, float* stats_inout,
+                                    const kge_adam_desc* adam, float* grad_entity, float* grad_relation,
+                                    float* grad_modulus, float* losses_out, void* workspace, size_t workspace_bytes,
+                                    int32_t* err_flag, void* stream, int32_t phases, int64_t entity_begin,
+                                    int64_t entity_end, int32_t csr_ready, int32_t reg_relations) {
+  if (phases <= 0 || phases > KGE_PHASE_ALL) return KGE_ERR_ARG;
+  if (entity_begin < 0 || entity_end < entity_begin || entity_end > (m ? m->nentity : 0)) return KGE_ERR_ARG;
+  return train_impl(m, mode, pos, neg, batch, nneg, subsampling_weight, weight_sum, uni_weight, uni_batch, 1, 1.f,
+                    regularization, adam, grad_entity, grad_relation, grad_modulus, losses_out, workspace,
+                    workspace_bytes, err_flag, stream, phases, entity_begin, entity_end,
+                    csr_ready ? XS_FROM_ROWS_CSR : XS_FROM_ROWS, const_cast<float*>(g_in), const_cast<float*>(dq_in),
+                    stats_inout, reg_relations ? 1 : 0);
+}
+
 int kge_train_csr(const kge_model_desc* m, int32_t mode, const int64_t* pos, const int64_t* neg, int64_t batch,
                   int64_t nneg, void* workspace, size_t workspace_bytes, int32_t* err_flag, void* stream) {
   return train_impl(m, mode, pos, neg, batch, nneg, nullptr, nullptr, 1, 0, 1, 1.f, 0.f, nullptr, nullptr, nullptr,

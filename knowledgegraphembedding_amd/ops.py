@@ -302,13 +302,15 @@ def train_step_from_rows(desc: _lib.ModelDesc, mode: str, pos: torch.Tensor, neg
                          grad_entity: torch.Tensor, grad_relation: torch.Tensor, grad_modulus: Optional[torch.Tensor],
                          losses: torch.Tensor, adam: Optional[_lib.AdamDesc] = None, csr_ready: bool = False,
                          workspace: Optional[torch.Tensor] = None, entity_range: Optional[tuple] = None,
-                         reg_relations: bool = True) -> None:
+                         reg_relations: bool = True, phases: Optional[int] = None) -> None:
     """The rest of the step for the whole (gathered) batch from the exchanged
     row factors (kge_train_step_from_rows; with csr_ready the CSR train_csr
     built for this batch, kge_train_step_from_rows_csr); bit-identical to one
     process running train_step_grads / the fused step on that batch.  With
     `entity_range` (e0, e1) the entity-major pass and its Adam cover only those
-    rows (the owner-computes step, kge_train_step_from_rows_range)."""
+    rows (the owner-computes step, kge_train_step_from_rows_range); with
+    `phases` as well, only those phases run (PHASE_ROWS / PHASE_ENTITY /
+    PHASE_FINALIZE, kge_train_step_from_rows_phased)."""
     if mode not in ("head-batch", "tail-batch"):
         raise ValueError("Training batch mode %s not supported" % mode)
     pos, neg = _idx(pos, dev), _idx(neg, dev)
@@ -321,6 +323,12 @@ def train_step_from_rows(desc: _lib.ModelDesc, mode: str, pos: torch.Tensor, neg
             int(bool(uni_weight)), int(uni_batch), float(regularization), g_in.data_ptr(), dq_in.data_ptr(),
             stats.data_ptr(), adam, grad_entity.data_ptr(), grad_relation.data_ptr(), _ptr(grad_modulus),
             losses.data_ptr(), ws.data_ptr(), ws.numel(), st.err.data_ptr(), _stream(dev))
+    if phases is not None:
+        e0, e1 = entity_range if entity_range is not None else (0, desc.nentity)
+        _lib.check(_lib.load().kge_train_step_from_rows_phased(*args, int(phases), int(e0), int(e1),
+                                                               int(bool(csr_ready)), int(bool(reg_relations))),
+                   "kge_train_step_from_rows_phased")
+        return
     if entity_range is not None:
         e0, e1 = entity_range
         _lib.check(_lib.load().kge_train_step_from_rows_range(*args, int(e0), int(e1), int(bool(csr_ready)),

@@ -47,13 +47,24 @@ slices a full-table state back to the shard.
 from __future__ import annotations
 
 import copy
+import os
 
 import torch
 import torch.distributed as dist
 from torch import nn
 
+from . import _lib
 from . import distributed as _dist
 from .distributed import dp_allreduce_, dp_weight_sum
+
+# owner-computes step: the owned rows' entity pass + Adam in this many chunks,
+# each chunk's all-gather overlapping the next chunk's pass (1 = one all-gather
+# after the whole step)
+OWNER_CHUNKS = int(os.environ.get("KGE_OWNER_CHUNKS", "4"))
+
+
+def _lib_phase(name: str) -> int:
+    return getattr(_lib, "PHASE_" + name)
 
 
 class EntityRowPartition:
@@ -96,6 +107,8 @@ class EntityRowPartition:
             model.fuse_optimizer = False  # Adam runs on the shard, not on the replica the kernel reads
         model.row_partition = self
         self.model = model
+        self._pending = []  # (all-gather work, staging buffer, shard rows c0, c1) of the owner step's chunks
+        self._stage = {}
 
     # ------------------------------------------------------------ parameters
     def parameters(self):
@@ -107,7 +120,17 @@ class EntityRowPartition:
         return [p for p in out if p.requires_grad]
 
     def gather(self) -> None:
-        """Refresh the replica from every rank's shard (all-gather)."""
+        """Refresh the replica from every rank's shard (all-gather).  After an
+        owner step whose chunks were already put on the wire
+        (_owner_step), wait for those and place them instead."""
+        if self._pending:
+            for work, stage, c0, c1 in self._pending:
+                work.wait()
+                # stage row r·(c1-c0) + j = rank r's shard row c0 + j
+                self.full.view(self.world, self.rows, self.dim)[:, c0:c1].copy_(
+                    stage.view(self.world, c1 - c0, self.dim))
+            self._pending = []
+            return
         src = self.shard.detach()
         if self.exchange == "factors":
             src = src.clone()  # the shard views the output: gather from a copy, never in place
@@ -156,11 +179,31 @@ class EntityRowPartition:
                                                 model.relation_embedding, model._modulus(),
                                                 write_grad=model.keep_grads)
         ge, gr, gm, losses = model._grad_buffers()  # ge = grad_full[:E]; rows [lo, hi) are written
-        ops.train_step_from_rows(model.desc(), mode, fx.pos, fx.neg, fx.w, fx.wsum, dev, uni_weight=fx.uni,
-                                 uni_batch=fx.B, regularization=float(args.regularization), g_in=fx.g, dq_in=fx.dq,
-                                 stats=fx.stats, grad_entity=ge, grad_relation=gr, grad_modulus=gm, losses=losses,
-                                 adam=adam, csr_ready=_dist.FX_CSR_AHEAD, workspace=fx.workspace,
-                                 entity_range=(self.lo, self.hi), reg_relations=self.rank == 0)
+        kw = dict(uni_weight=fx.uni, uni_batch=fx.B, regularization=float(args.regularization), g_in=fx.g,
+                  dq_in=fx.dq, stats=fx.stats, grad_entity=ge, grad_relation=gr, grad_modulus=gm, losses=losses,
+                  adam=adam, csr_ready=_dist.FX_CSR_AHEAD, workspace=fx.workspace, reg_relations=self.rank == 0)
+        desc = model.desc()
+        chunks = self._owner_chunks() if adam is not None else []
+        if len(chunks) <= 1:
+            ops.train_step_from_rows(desc, mode, fx.pos, fx.neg, fx.w, fx.wsum, dev, entity_range=(self.lo, self.hi),
+                                     **kw)
+        else:
+            # the entity pass + fused Adam of the owned rows in chunks; chunk
+            # c's all-gather (every rank's rows c0..c1 of its shard) is on the
+            # wire while chunk c+1 is computed; gather() places them
+            ops.train_step_from_rows(desc, mode, fx.pos, fx.neg, fx.w, fx.wsum, dev, entity_range=(self.lo, self.hi),
+                                     phases=_lib_phase("ROWS"), **kw)
+            for c0, c1 in chunks:
+                e0, e1 = self.lo + c0, min(self.hi, self.lo + c1)
+                if e1 > e0:
+                    ops.train_step_from_rows(desc, mode, fx.pos, fx.neg, fx.w, fx.wsum, dev, entity_range=(e0, e1),
+                                             phases=_lib_phase("ENTITY"), **kw)
+                stage = self._stage_buf(c0, c1 - c0, dev)  # one buffer per chunk: the gathers overlap
+                work = dist.all_gather_into_tensor(stage, self.full[self.lo + c0:self.lo + c1], group=self.group,
+                                                   async_op=True)
+                self._pending.append((work, stage, c0, c1))
+            ops.train_step_from_rows(desc, mode, fx.pos, fx.neg, fx.w, fx.wsum, dev, entity_range=(self.lo, self.hi),
+                                     phases=_lib_phase("FINALIZE"), **kw)
         # the owner's rows of the gradient; the replica itself is not optimised
         self.shard.grad = self.grad_full[self.lo:self.lo + self.rows] if adam is None or model.keep_grads else None
         model.entity_embedding.grad = None
@@ -172,6 +215,20 @@ class EntityRowPartition:
             dist.all_reduce(losses[3:4], op=dist.ReduceOp.SUM, group=self.group)
             losses[2] = (losses[0] + losses[1]) / 2 + losses[3]
         return losses
+
+    def _owner_chunks(self):
+        """Shard row ranges [c0, c1) of the chunked owner step (OWNER_CHUNKS
+        equal pieces of the padded shard; one piece when the shard is small)."""
+        k = max(1, min(OWNER_CHUNKS, self.rows // 32))
+        step = -(-self.rows // k)
+        return [(c0, min(self.rows, c0 + step)) for c0 in range(0, self.rows, step)]
+
+    def _stage_buf(self, c0: int, nrows: int, dev) -> torch.Tensor:
+        key = (c0, nrows, dev)
+        b = self._stage.get(key)
+        if b is None:
+            b = self._stage[key] = torch.empty(self.world * nrows, self.dim, device=dev)
+        return b
 
     # ------------------------------------------------------------ checkpoints
     def _gather_rows(self, t: torch.Tensor) -> torch.Tensor:

@@ -53,11 +53,13 @@ def _args(group, reg, uni):
                      regularization=reg, dp_group=group)
 
 
-def _worker(rank, world, port, name, reg, uni, out):
+def _worker(rank, world, port, name, reg, uni, chunks, out):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     torch.cuda.set_device(0)
     dist.init_process_group("gloo", rank=rank, world_size=world)
+    from knowledgegraphembedding_amd import partition
     from knowledgegraphembedding_amd.partition import EntityRowPartition
+    partition.OWNER_CHUNKS = chunks
     model = _model(name)
     part = EntityRowPartition(model, dist.group.WORLD, exchange="factors")
     opt = KGEAdam(part.parameters(), lr=LR)
@@ -74,12 +76,17 @@ def _worker(rank, world, port, name, reg, uni, out):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("name,reg,uni,world", [("RotatE", 0.0, False, 2), ("RotatE", 0.0, False, 4),
-                                                ("ComplEx", 1e-4, False, 4), ("pRotatE", 0.0, True, 2),
-                                                ("TransE", 0.0, False, 4), ("DistMult", 1e-4, True, 2)])
-def test_owner_exchange_bitwise(name, reg, uni, world):
+@pytest.mark.parametrize("name,reg,uni,world,chunks", [("RotatE", 0.0, False, 2, 4), ("RotatE", 0.0, False, 4, 4),
+                                                       ("RotatE", 0.0, False, 2, 1), ("ComplEx", 1e-4, False, 4, 4),
+                                                       ("pRotatE", 0.0, True, 2, 4), ("TransE", 0.0, False, 4, 1),
+                                                       ("DistMult", 1e-4, True, 2, 3)])
+def test_owner_exchange_bitwise(name, reg, uni, world, chunks):
+    """chunks > 1: the owned rows' pass in chunks (kge_train_step_from_rows_phased),
+    each chunk's all-gather issued before the next chunk runs (151 owned rows
+    at world 2 give 4 chunks, 76 at world 4 give 2); 1: one call and one
+    all-gather.  Both bit-identical to one process."""
     out = mp.Manager().dict()
-    mp.spawn(_worker, args=(world, _free_port(), name, reg, uni, out), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), name, reg, uni, chunks, out), nprocs=world, join=True)
     model = _model(name)
     opt = KGEAdam([p for p in model.parameters() if p.requires_grad], lr=LR)
     it = iter(_batches("cuda:0"))
