@@ -11,11 +11,8 @@
 // are produced by identical instruction sequences and compare consistently.
 //
 // Tile: 128 queries × 128 candidates per workgroup (4 waves as 2×2, each
-// 64×64 = 2×2 MFMA tiles), K staged through LDS 32 deep, rows kept row-major
-// with each 8-k group permuted into MFMA consumption order, so one
-// ds_read_b128 per operand feeds four k-steps; the next slab's global loads
-// are issued into registers before the current slab's MFMAs, so their
-// latency hides behind the matrix work.
+// 64×64 = 2×2 MFMA tiles), K staged through LDS 16 deep by LDS-DMA into two
+// alternating buffers (details at k_rank_mfma).
 // Candidates are the MFMA rows and queries the columns, so each lane owns two
 // query columns: the epilogue tests its 32 candidates per query against s_true
 // and a 2-word slice of the query's exclusion bitmap (filtered ids, the true
@@ -24,6 +21,8 @@
 // exact and order-free.  Candidates within the query's near-tie window are not
 // counted but listed (win_count) for the reference-order refinement
 // (kge_rank_ref.h): the fma order here is not the reference's sum order.
+#include <cstdlib>
+
 #include "kge_common.h"
 
 namespace kge {
@@ -32,12 +31,7 @@ namespace {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
-constexpr int BM = 128, BN = 128, BK = 32;
-// LDS slab: row-major [128 rows][LDK], each group of 8 k stored in MFMA
-// consumption order [k0, k0+2, k0+4, k0+6 | k0+1, k0+3, k0+5, k0+7] so one
-// ds_read_b128 gives a lane (row li, half kh) its operands for 4 k-steps.
-constexpr int LDK = BK + 4;
-constexpr int F4 = (BM * BK / 4) / 256;  // float4 per thread per operand per slab
+constexpr int BM = 128, BN = 128;
 
 struct MfmaArgs {
   const float* q;        // [nq, K]
@@ -52,49 +46,35 @@ struct MfmaArgs {
   RankWin win;
 };
 
-// One [128 rows × BK] slab of row-major [*, K] data: thread t holds float4
-// f = t + 256u (row f / (BK/4), k = (f % (BK/4))·4 .. +3) in registers
-// (fetch), then writes it transposed into LDS as [k][row] (put).
-__device__ __forceinline__ void fetch(float4 (&r)[F4], const float* __restrict__ src, const int64_t* rows, int K,
-                                      int k0, int t) {
-#pragma unroll
-  for (int u = 0; u < F4; ++u) {
-    const int f = t + 256 * u;
-    const int row = f / (BK / 4), kq = (f % (BK / 4)) * 4;
-    const int64_t gr = rows[row];
-    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (gr >= 0) {
-      const float* p = src + gr * (int64_t)K + k0 + kq;
-      if (k0 + kq + 3 < K) {
-        v = *reinterpret_cast<const float4*>(p);
-      } else {
-        if (k0 + kq + 0 < K) v.x = p[0];
-        if (k0 + kq + 1 < K) v.y = p[1];
-        if (k0 + kq + 2 < K) v.z = p[2];
-      }
-    }
-    r[u] = v;
-  }
-}
-__device__ __forceinline__ void put(float (*dst)[LDK], const float4 (&r)[F4], int t) {
-#pragma unroll
-  for (int u = 0; u < F4; ++u) {
-    const int f = t + 256 * u;
-    const int row = f / (BK / 4), kq = (f % (BK / 4)) * 4;
-    // k = kq..kq+3 → positions (k & 1)·4 + ((k & 7) >> 1) inside the 8-group
-    const int base = (kq & ~7) + ((kq & 4) ? 2 : 0);
-    *reinterpret_cast<float2*>(&dst[row][base]) = make_float2(r[u].x, r[u].z);
-    *reinterpret_cast<float2*>(&dst[row][base + 4]) = make_float2(r[u].y, r[u].w);
-  }
-}
+// The tile's K slabs go global → LDS by LDS-DMA
+// (buffer_load_dwordx4 … lds: no staging VGPRs, no LDS write pass), 16 deep
+// and double-buffered, so each slab costs one barrier and its loads run behind
+// the previous slab's MFMAs; 36 KB of LDS and ≤ 128 VGPRs give 4 workgroups
+// per CU.  The DMA image is lane-linear (16 rows × 64 B per wave-instruction),
+// so the k order inside an MFMA step is chosen to read contiguous 16-B chunks:
+// step u of 8-group g pairs k = 8g + u (lanes 0-31) with k = 8g + 4 + u
+// (lanes 32-63), and each row's four 16-B chunks are XOR-swizzled by
+// (row >> 2) & 3 on the SOURCE address, which makes every ds_read_b128 of the
+// operand fragments conflict-free.  Rows past nq / E and k ≥ K read as zero
+// (buffer range check), so edge tiles need no selects.  Same epilogue as v1;
+// the fast score's fma order differs from v1 (the near-tie window bounds any
+// order, and the gather pass runs the same kernel).  An earlier version
+// staged 32-deep slabs through registers with two barriers per slab (158
+// VGPRs, 3 workgroups per CU): 68 % MFMA-busy against 79 % here.
+constexpr int BK2 = 16;
+constexpr int STAGE2 = 2 * 128 * BK2;  // floats per stage: A [128][16] then B [128][16]
+constexpr uint32_t OOB2 = 0x7FFFFFF0u;
 
 template <bool GATHER>
-__global__ __launch_bounds__(256, 3) void k_rank_mfma(MfmaArgs a) {
-  __shared__ __attribute__((aligned(16))) float As[BM][LDK];
-  __shared__ __attribute__((aligned(16))) float Bs[BN][LDK];
-  __shared__ int64_t arow[128], brow[128];
-  __shared__ float sts[128], sdl[128];
-  __shared__ int32_t cgt[128];
+__global__ __launch_bounds__(256, 4) void k_rank_mfma(MfmaArgs a) {
+  // one LDS array (a second __shared__ object can cost a vmcnt(0) per k-step):
+  // [2 stages][A | B] slabs, then arow/brow (int64), sts, sdl, cgt
+  __shared__ __attribute__((aligned(16))) float smem[2 * STAGE2 + 128 * 2 + 128 * 2 + 128 * 3];
+  int64_t* arow = reinterpret_cast<int64_t*>(smem + 2 * STAGE2);
+  int64_t* brow = arow + 128;
+  float* sts = reinterpret_cast<float*>(brow + 128);
+  float* sdl = sts + 128;
+  int32_t* cgt = reinterpret_cast<int32_t*>(sdl + 128);
   const int t = threadIdx.x, lane = t & 63, w = wave_id();
   const int wm = w >> 1, wn = w & 1;
   const int64_t q0 = (int64_t)blockIdx.y * BM;
@@ -115,6 +95,35 @@ __global__ __launch_bounds__(256, 3) void k_rank_mfma(MfmaArgs a) {
   }
   __syncthreads();
 
+  const auto rq = buf_rsrc(a.q, (uint64_t)a.nq * a.K * 4u);
+  const auto re = buf_rsrc(a.ent, (uint64_t)a.E * a.K * 4u);
+  // this lane's DMA pieces: wave-instruction t2 ∈ {2w, 2w+1} of each operand
+  // covers rows 16·t2 .. +15, lane l → row 16·t2 + l/4, LDS chunk p = l & 3,
+  // source chunk p ^ ((row >> 2) & 3)
+  int64_t growA[2], growB[2];
+  int cpos[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int row = 16 * (2 * w + h) + (lane >> 2);
+    growA[h] = arow[row];
+    growB[h] = brow[row];
+    cpos[h] = (lane & 3) ^ ((row >> 2) & 3);
+  }
+  auto issue = [&](int k0, int stage) {
+    float* base = smem + stage * STAGE2;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int kk = k0 + 4 * cpos[h];
+      const bool kin = kk < a.K;
+      const uint32_t oa = (kin && growA[h] >= 0) ? (uint32_t)((growA[h] * a.K + kk) * 4) : OOB2;
+      const uint32_t ob = (kin && growB[h] >= 0) ? (uint32_t)((growB[h] * a.K + kk) * 4) : OOB2;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rq, (__attribute__((address_space(3))) void*)(base + (2 * w + h) * 256),
+                                               16, oa, 0, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          re, (__attribute__((address_space(3))) void*)(base + 128 * BK2 + (2 * w + h) * 256), 16, ob, 0, 0, 0);
+    }
+  };
+
   f32x16 acc[2][2];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
@@ -124,28 +133,27 @@ __global__ __launch_bounds__(256, 3) void k_rank_mfma(MfmaArgs a) {
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
   const int kh = lane >> 5, li = lane & 31;
-  float4 ra[F4], rb[F4];
-  fetch(ra, a.q, arow, a.K, 0, t);
-  fetch(rb, a.ent, brow, a.K, 0, t);
-  for (int k0 = 0; k0 < a.K; k0 += BK) {
-    put(As, ra, t);
-    put(Bs, rb, t);
-    __syncthreads();
-    if (k0 + BK < a.K) {  // next slab's global loads in flight behind the MFMAs
-      fetch(ra, a.q, arow, a.K, k0 + BK, t);
-      fetch(rb, a.ent, brow, a.K, k0 + BK, t);
-    }
+  const int nslab = (a.K + BK2 - 1) / BK2;
+  issue(0, 0);
+  for (int s = 0; s < nslab; ++s) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA of slab s has landed
+    __syncthreads();                                   // ... every wave's; slab s-1's reads are done
+    if (s + 1 < nslab) issue((s + 1) * BK2, (s + 1) & 1);
+    const float* As = smem + (s & 1) * STAGE2;
+    const float* Bs = As + 128 * BK2;
 #pragma unroll
-    for (int g = 0; g < BK / 8; ++g) {
-      // k order: step 4g + u takes k = k0 + 8g + 2u (lanes 0-31) and + 1
-      // (lanes 32-63) — ascending k across the loop, the same in both passes.
-      // Candidates are the MFMA rows (A), queries the columns (B): a lane's
-      // accumulator column is one query, so the epilogue counts per lane.
+    for (int g = 0; g < BK2 / 8; ++g) {
       float4 e4[2], q4[2];
 #pragma unroll
-      for (int i = 0; i < 2; ++i) e4[i] = *reinterpret_cast<const float4*>(&Bs[wm * 64 + i * 32 + li][g * 8 + kh * 4]);
+      for (int i = 0; i < 2; ++i) {
+        const int row = wm * 64 + i * 32 + li;
+        e4[i] = *reinterpret_cast<const float4*>(Bs + row * BK2 + 4 * ((2 * g + kh) ^ ((row >> 2) & 3)));
+      }
 #pragma unroll
-      for (int j = 0; j < 2; ++j) q4[j] = *reinterpret_cast<const float4*>(&As[wn * 64 + j * 32 + li][g * 8 + kh * 4]);
+      for (int j = 0; j < 2; ++j) {
+        const int row = wn * 64 + j * 32 + li;
+        q4[j] = *reinterpret_cast<const float4*>(As + row * BK2 + 4 * ((2 * g + kh) ^ ((row >> 2) & 3)));
+      }
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         const float ef[2] = {u == 0 ? e4[0].x : u == 1 ? e4[0].y : u == 2 ? e4[0].z : e4[0].w,
@@ -159,13 +167,10 @@ __global__ __launch_bounds__(256, 3) void k_rank_mfma(MfmaArgs a) {
             acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(ef[i], qf[j], acc[i][j], 0, 0, 0);
       }
     }
-    __syncthreads();
   }
 
   // C/D layout: col (query) = lane & 31, row (candidate) = (reg & 3) + 8·(reg >> 2) + 4·(lane >> 5)
   if (GATHER) {
-    // diagonal: candidate row m == query column n; for column li that is
-    // register r = 4·(li >> 3) + (li & 3) of the lane half kh = (li >> 2) & 1
     if (wm != wn || kh != ((li >> 2) & 1)) return;
     const int rd = 4 * (li >> 3) + (li & 3);
 #pragma unroll
@@ -177,14 +182,12 @@ __global__ __launch_bounds__(256, 3) void k_rank_mfma(MfmaArgs a) {
     }
     return;
   }
-  const int64_t wbase = e0 >> 5;  // the tile's 128 candidates = bitmap words wbase .. wbase+3
+  const int64_t wbase = e0 >> 5;
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     const int n = wn * 64 + j * 32 + li;
     const int64_t q = arow[n];
     const float st = sts[n], dlt = sdl[n];
-    // excluded candidates of this query among rows wm·64 .. +63: filtered ids
-    // and the true id (bitmap), and ids past E
     uint32_t ex[2];
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
@@ -205,12 +208,11 @@ __global__ __launch_bounds__(256, 3) void k_rank_mfma(MfmaArgs a) {
         const float sc = acc[i][j][r];
         const float diff = sc - st;
         g += (ok && diff > dlt) ? 1 : 0;
-        if (ok && !(diff > dlt) && diff >= -dlt) {  // near tie: listed, not counted
+        if (ok && !(diff > dlt) && diff >= -dlt) {
           const int idx = atomicAdd(&a.win.ucnt[q], 1);
           if (idx < a.win.cap) a.win.ulist[q * (int64_t)a.win.cap + idx] = (int32_t)(e0 + wm * 64 + i * 32 + mloc);
         }
       }
-    // lanes l and l + 32 hold the two row halves of the same query column
     g += __shfl_xor(g, 32);
     if (kh == 0 && q >= 0 && g) atomicAdd(&cgt[n], g);
   }
@@ -281,6 +283,8 @@ int launch_rank_mfma(int gather, const float* q, const float* ent, int64_t nq, i
   const unsigned gy = (unsigned)((nq + BM - 1) / BM);
   // 3 waves/SIMD (158 VGPRs, no spills); 4 fits only with 13 spilled VGPRs
   // and measured 12 % slower
+  // buffer offsets are 32-bit: both operands must stay below 4 GB
+  if ((uint64_t)E * K * 4 >= 0xFFFFFF00ull || (uint64_t)nq * K * 4 >= 0xFFFFFF00ull) return -1;
   if (gather) {
     hipLaunchKernelGGL((k_rank_mfma<true>), dim3(1, gy), dim3(256), 0, s, a);
   } else {
@@ -336,8 +340,8 @@ __global__ __launch_bounds__(256) void k_table_stats(const float* __restrict__ e
 int launch_table_stats(const float* ent, int64_t E, int Le, float* stats, hipStream_t s) {
   hipError_t e = hipMemsetAsync(stats, 0, 2 * sizeof(float), s);
   if (e != hipSuccess) return (int)e;
-  const int64_t blocks = (E + 3) / 4;  // one row per wave: every row in flight at once
-  hipLaunchKernelGGL(k_table_stats, dim3((unsigned)(blocks < 65535 ? blocks : 65535)), dim3(256), 0, s, ent, E, Le,
+  const int64_t blocks = (E + 3) / 4;  // ≤ 512 blocks: one atomic pair per block
+  hipLaunchKernelGGL(k_table_stats, dim3((unsigned)(blocks < 512 ? blocks : 512)), dim3(256), 0, s, ent, E, Le,
                      stats);
   return (int)hipGetLastError();
 }
