@@ -198,10 +198,7 @@ class EntityRowPartition:
                 if e1 > e0:
                     ops.train_step_from_rows(desc, mode, fx.pos, fx.neg, fx.w, fx.wsum, dev, entity_range=(e0, e1),
                                              phases=_lib_phase("ENTITY"), **kw)
-                stage = self._stage_buf(c0, c1 - c0, dev)  # one buffer per chunk: the gathers overlap
-                work = dist.all_gather_into_tensor(stage, self.full[self.lo + c0:self.lo + c1], group=self.group,
-                                                   async_op=True)
-                self._pending.append((work, stage, c0, c1))
+                self.put_chunk(c0, c1)
             ops.train_step_from_rows(desc, mode, fx.pos, fx.neg, fx.w, fx.wsum, dev, entity_range=(self.lo, self.hi),
                                      phases=_lib_phase("FINALIZE"), **kw)
         # the owner's rows of the gradient; the replica itself is not optimised
@@ -215,6 +212,16 @@ class EntityRowPartition:
             dist.all_reduce(losses[3:4], op=dist.ReduceOp.SUM, group=self.group)
             losses[2] = (losses[0] + losses[1]) / 2 + losses[3]
         return losses
+
+    def put_chunk(self, c0: int, c1: int) -> None:
+        """Start the all-gather of every rank's shard rows [c0, c1) (collective,
+        async): rank r's rows land at stage rows r·(c1−c0) …, gather() waits and
+        places them at replica rows r·S + c0 ….  One staging buffer per chunk,
+        so the gathers of consecutive chunks can be on the wire together."""
+        stage = self._stage_buf(c0, c1 - c0, self.full.device)
+        work = dist.all_gather_into_tensor(stage, self.full[self.lo + c0:self.lo + c1], group=self.group,
+                                           async_op=True)
+        self._pending.append((work, stage, c0, c1))
 
     def _owner_chunks(self):
         """Shard row ranges [c0, c1) of the chunked owner step (OWNER_CHUNKS
