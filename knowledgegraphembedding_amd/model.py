@@ -17,6 +17,7 @@ tensors are rejected instead of silently falling back.
 from __future__ import annotations
 
 import logging
+import time
 
 import numpy as np
 import torch
@@ -32,11 +33,16 @@ class StepLog(dict):
     """train_step's log — the reference's {name: float} dict (model.py:305-312)
     — filled from the device on first read.
 
-    The step's four losses and the device error flag are copied into a pinned
-    host slot behind an event; reading any key (or iterating, printing, json
-    dumping) waits for that event and raises the deferred error if the step
-    saw an out-of-range index.  Until then the host is free to enqueue the
-    next step, so the GPU does not idle while Python prepares it."""
+    The step's four losses and the device error flag land in a pinned host
+    slot — written there by the single-device step's k_finalize itself, or
+    copied behind an event by the multi-GPU steps; reading any key (or
+    iterating, printing, json dumping) waits for them and raises the deferred
+    error if the step saw an out-of-range index.  Until then the host is free
+    to enqueue the next step, so the GPU does not idle while Python prepares
+    it.  A slot the kernel writes directly is pre-filled with NaN and polled
+    (no event: a marker after every step cost ~6 µs of device time); after
+    POLL_SPIN_S without all five values the read falls back to a device
+    synchronize, so a NaN loss is still reported correctly."""
 
     __slots__ = ('_src',)
 
@@ -52,6 +58,8 @@ class StepLog(dict):
         host, event, has_reg, dev = src
         if event is not None:
             event.synchronize()
+        elif host.is_pinned():
+            _poll_slot(host, dev)
         vals = host.tolist()
         if vals[4] != 0.0:  # device error flag (out-of-range index), copied by the kernels
             ops.raise_on_device_error(dev)
@@ -110,6 +118,23 @@ class StepLog(dict):
         return (dict, (dict(self.items()),))
 
 
+POLL_SPIN_S = 0.05
+
+
+def _poll_slot(host: torch.Tensor, dev) -> None:
+    """Wait until k_finalize's five floats replaced the NaN sentinel in the
+    pinned slot (each is written once, so five non-NaN values are final), or
+    synchronize the device after POLL_SPIN_S (a NaN loss, a slow step)."""
+    arr = host.numpy()
+    if not np.isnan(arr).any():
+        return
+    t0 = time.perf_counter()
+    while np.isnan(arr).any():
+        if time.perf_counter() - t0 > POLL_SPIN_S:
+            torch.cuda.synchronize(dev)
+            return
+
+
 class _LogRing:
     """Pinned host slots for the per-step loss read-back.  Reusing a slot first
     completes the log that occupied it, so the host runs at most len(slots)
@@ -130,6 +155,7 @@ class _LogRing:
         if slot[2] is not None:
             slot[2]._fill()
             slot[2] = None
+        slot[0].fill_(float('nan'))  # the sentinel the log polls for (a host write: the slot is pinned memory)
         return slot[0]
 
     def push(self, losses: torch.Tensor, has_reg: bool) -> StepLog:
@@ -139,11 +165,14 @@ class _LogRing:
         self.k = (self.k + 1) % len(self.slots)
         if slot[2] is not None:
             slot[2]._fill()
-        if losses.data_ptr() != slot[0].data_ptr():
+        direct = losses.data_ptr() == slot[0].data_ptr()  # k_finalize wrote the reserved slot itself
+        if not direct:
             slot[0].copy_(losses, non_blocking=True)
-        if slot[1] is not None:
+        event = None
+        if slot[1] is not None and not direct:
             slot[1].record()
-        log = StepLog((slot[0], slot[1], has_reg, self.dev))
+            event = slot[1]
+        log = StepLog((slot[0], event, has_reg, self.dev))
         slot[2] = log
         return log
 
