@@ -72,7 +72,9 @@ int rank_path(const kge_model_desc* m, int requested) {
   const bool cplx = (m->model == KGE_ROTATE || m->model == KGE_COMPLEX);
   const int K = cplx ? m->entity_dim / 2 : m->entity_dim;
   const bool al = aligned16(m->entity_embedding);
-  const bool mfma_ok = bil && (m->entity_dim % 4 == 0) && al;
+  // (the MFMA tile addresses the table through 32-bit buffer offsets)
+  const bool mfma_ok = bil && (m->entity_dim % 4 == 0) && al &&
+                       (uint64_t)m->nentity * (uint64_t)m->entity_dim * 4u < 0xFFFFFF00ull;
   const bool tile_ok = (K % 4 == 0) && al;
   if (requested == RP_MFMA) return mfma_ok ? RP_MFMA : -1;
   if (requested == RP_TILE) return tile_ok ? RP_TILE : -1;
