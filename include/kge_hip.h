@@ -287,6 +287,61 @@ int kge_train_step_from_rows_phased(const kge_model_desc *m, int32_t mode, const
                                     int32_t *err_flag, void *stream, int32_t phases, int64_t entity_begin,
                                     int64_t entity_end, int32_t csr_ready, int32_t reg_relations);
 
+/*
+ * Query shipping: the training step of model.py:252-312 with the entity table
+ * split into row shards, one per rank (no rank holds another's rows — the
+ * reference's single table, model.py:45-53, never exists as a whole).  The
+ * ranks exchange the global batch's ids and q vectors, not rows; every row-
+ * side term is computed by the owner of the row.  The model descriptor's
+ * entity_embedding points own_begin rows before this rank's shard and its
+ * nentity is the GLOBAL entity count; the Adam entity pointers (and
+ * grad_entity) are offset the same way.  Stages, each a call with the same
+ * arguments, with the host's collectives between them:
+ *   KGE_SHIP_Q      q_i (and head-batch the positive's h∘r) from the owner
+ *                   of its row, zero elsewhere         → all-reduce(SUM) q[, qp]
+ *   KGE_SHIP_ROWS   the owned negatives of every row: partial softmax state,
+ *                   V relative to this shard's max (and the occurrence CSR,
+ *                   on a side stream)                  → all-gather part → parts
+ *   KGE_SHIP_MERGE  the rows' softmax over the shards (shard order), this
+ *                   shard's dL/dq share and dL/ds; the positive triple on the
+ *                   owner of t                         → all-reduce(SUM) dq | pstats [| pq]
+ *   KGE_SHIP_CHAIN  chain rule on the owners of h / t; this shard's part of the
+ *                   relation gradient (regulariser on rank 0) into
+ *                   grad_relation                      → all-reduce(SUM) grad_relation,
+ *                   relation Adam by the caller
+ *   KGE_SHIP_ENTITY entity-major pass + fused Adam over [own_begin, own_end),
+ *                   losses (regulariser partial of the owned rows; of the
+ *                   relations on rank 0 only), pRotatE modulus grad + Adam
+ * Same maths as one process on the global batch; the cross-shard sums run in
+ * another order, so results agree to fp32 rounding, not bit for bit.
+ */
+#define KGE_SHIP_Q 1
+#define KGE_SHIP_ROWS 2
+#define KGE_SHIP_MERGE 3
+#define KGE_SHIP_CHAIN 4
+#define KGE_SHIP_ENTITY 5
+typedef struct kge_ship_desc {
+  int32_t world, rank;
+  int64_t own_begin, own_end;       /* entity rows this rank owns (global ids) */
+  const int64_t *pos, *neg;         /* [B,3], [B,n] the global batch (all ranks' rows, rank order) */
+  int64_t batch, nneg;              /* B (global), n */
+  const float *subsampling_weight;  /* [B] */
+  const float *weight_sum;          /* global Σw (device scalar; unused with uni_weight) */
+  int32_t uni_weight, adversarial;
+  int64_t uni_batch;
+  float adversarial_temperature, regularization;
+  float *q, *qp;                    /* [B, Le] each; qp: head-batch only */
+  float *part;                      /* [B, 4] */
+  const float *parts;               /* [world, B, 4] */
+  float *scores, *g;                /* [B, n] each */
+  float *dq, *pq, *pstats;          /* [B, Le], [B, Le] (head-batch), [B, 4] */
+  float *ent_contrib, *rel_contrib; /* [2B, Le], [B, Lr] */
+  float *row_stats;                 /* [B, 4] */
+} kge_ship_desc;
+int kge_ship_step(const kge_model_desc *m, int32_t mode, const kge_ship_desc *ship, int32_t stage,
+                  const kge_adam_desc *adam, float *grad_entity, float *grad_relation, float *grad_modulus,
+                  float *losses_out, void *workspace, size_t workspace_bytes, int32_t *err_flag, void *stream);
+
 
 /*
  * Σ subsampling_weight into *out (device scalar) — the denominator of

@@ -18,6 +18,7 @@ MODE_IDS = {"single": 0, "head-batch": 1, "tail-batch": 2}
 DEVERR_INDEX = 1
 DEVERR_SAMPLER = 2
 PHASE_ROWS, PHASE_ENTITY, PHASE_FINALIZE, PHASE_ALL = 1, 2, 4, 7
+SHIP_Q, SHIP_ROWS, SHIP_MERGE, SHIP_CHAIN, SHIP_ENTITY = 1, 2, 3, 4, 5
 ERR_HIP_BASE = 1000
 
 
@@ -53,6 +54,19 @@ class AdamDesc(C.Structure):
 
     _fields_ = [("entity", AdamTensor), ("relation", AdamTensor), ("modulus", AdamTensor),
                 ("beta1", C.c_float), ("beta2", C.c_float), ("eps", C.c_float), ("write_grad", C.c_int32)]
+
+
+class ShipDesc(C.Structure):
+    """struct kge_ship_desc (query shipping, kge_ship_step)."""
+
+    _fields_ = [("world", C.c_int32), ("rank", C.c_int32), ("own_begin", C.c_int64), ("own_end", C.c_int64),
+                ("pos", C.c_void_p), ("neg", C.c_void_p), ("batch", C.c_int64), ("nneg", C.c_int64),
+                ("subsampling_weight", C.c_void_p), ("weight_sum", C.c_void_p), ("uni_weight", C.c_int32),
+                ("adversarial", C.c_int32), ("uni_batch", C.c_int64), ("adversarial_temperature", C.c_float),
+                ("regularization", C.c_float), ("q", C.c_void_p), ("qp", C.c_void_p), ("part", C.c_void_p),
+                ("parts", C.c_void_p), ("scores", C.c_void_p), ("g", C.c_void_p), ("dq", C.c_void_p),
+                ("pq", C.c_void_p), ("pstats", C.c_void_p), ("ent_contrib", C.c_void_p),
+                ("rel_contrib", C.c_void_p), ("row_stats", C.c_void_p)]
 
 
 _P = C.c_void_p
@@ -110,6 +124,8 @@ SIGNATURES = {
         [_DESC, _I32, _P, _P, _I64, _I64, _P, _P, _I32, _I64, _F, _P, _P, _P, C.POINTER(AdamDesc), _P, _P, _P, _P,
          _P, _SZ, _P, _P],
     ),
+    "kge_ship_step": (C.c_int, [_DESC, _I32, C.POINTER(ShipDesc), _I32, C.POINTER(AdamDesc), _P, _P, _P, _P, _P,
+                                _SZ, _P, _P]),
     "kge_weight_sum": (C.c_int, [_P, _I64, _P, _P]),
     "kge_adam_step": (C.c_int, [_P, _P, _P, _P, _I64, _F, _F, _F, _F, _F, _P]),
     "kge_rank_workspace_bytes": (_SZ, [_DESC, _I64]),

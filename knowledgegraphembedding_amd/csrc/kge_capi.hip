@@ -194,6 +194,28 @@ Side* side_for_device() {
 // XS_FROM_ROWS_CSR: XS_FROM_ROWS with that CSR already in the workspace
 enum XStage : int { XS_NONE = 0, XS_ROWS_ONLY = 1, XS_FROM_ROWS = 2, XS_CSR_ONLY = 3, XS_FROM_ROWS_CSR = 4 };
 
+// entity pass variant: column slices (k_entity_sl) when the row fits one
+// 16-B slot per lane per slice (returns the slice count); 0 selects the
+// row-per-wave pass (also forced by KGE_ENT_SLICES=0)
+int entity_slices(const Geom& geo, int64_t B, int Le) {
+  const int forced = env_int("KGE_ENT_SLICES", -1);  // read per call (tests switch it)
+  const int S = geo.eg.S;
+  auto fits = [&](int k) { return (S + k - 1) / k <= 64; };
+  if (geo.vec != 4 || forced == 0) return 0;
+  int k = forced;
+  if (k < 0) {
+    // smallest power of two that fits; doubled further while the q column
+    // slice exceeds 2 MiB (half an XCD L2) only if the waves stay >= 3/4
+    // busy (measured: a larger slice beats half-empty waves — global batch
+    // of 2048 rows, 4 slices 0.54 ms vs 8 slices 0.73 ms)
+    const double qslice = (double)B * Le * sizeof(float);
+    k = 1;
+    while (k < 8 && !fits(k)) k *= 2;
+    while (k < 8 && qslice / k > 2.0 * 1024 * 1024 && (S + 2 * k - 1) / (2 * k) >= 48) k *= 2;
+  }
+  return ((k == 1 || k == 2 || k == 4 || k == 8) && fits(k)) ? k : 0;
+}
+
 // Shared body of backward and train.  Caller's stream: q build → gather loop →
 // epilogue → entity pass → finalise; side stream: CSR ∥ row pass, relation pass ∥ entity pass.
 int run_grad(const kge_model_desc* m, const Geom& geo, int mode, const int64_t* pos, const int64_t* neg,
@@ -234,28 +256,7 @@ int run_grad(const kge_model_desc* m, const Geom& geo, int mode, const int64_t* 
   hipStream_t ss = sd ? sd->s : s;
   int st;
 
-  // entity pass variant: column slices (k_entity_sl) when the row fits one
-  // 16-B slot per lane per slice; KGE_ENT_SLICES=0 selects the row-per-wave pass
-  int nsl = 0;
-  {
-    const int forced = env_int("KGE_ENT_SLICES", -1);  // read per call (tests switch it)
-    const int S = geo.eg.S;
-    auto fits = [&](int k) { return (S + k - 1) / k <= 64; };
-    if (geo.vec == 4 && forced != 0) {
-      int k = forced;
-      if (k < 0) {
-        // smallest power of two that fits; doubled further while the q column
-        // slice exceeds 2 MiB (half an XCD L2) only if the waves stay >= 3/4
-        // busy (measured: a larger slice beats half-empty waves — global batch
-        // of 2048 rows, 4 slices 0.54 ms vs 8 slices 0.73 ms)
-        const double qslice = (double)B * Le * sizeof(float);
-        k = 1;
-        while (k < 8 && !fits(k)) k *= 2;
-        while (k < 8 && qslice / k > 2.0 * 1024 * 1024 && (S + 2 * k - 1) / (2 * k) >= 48) k *= 2;
-      }
-      if ((k == 1 || k == 2 || k == 4 || k == 8) && fits(k)) nsl = k;
-    }
-  }
+  const int nsl = entity_slices(geo, B, Le);
   const int64_t ent_parts = m->nentity * (int64_t)(nsl > 0 ? nsl : 1);
   // relation pass: as trailing blocks of the sliced entity launch (one call,
   // no stream join); else beside the entity pass on the side stream (always
@@ -630,6 +631,149 @@ int kge_train_step_from_rows_phased(const kge_model_desc* m, int32_t mode, const
                     workspace_bytes, err_flag, stream, phases, entity_begin, entity_end,
                     csr_ready ? XS_FROM_ROWS_CSR : XS_FROM_ROWS, const_cast<float*>(g_in), const_cast<float*>(dq_in),
                     stats_inout, reg_relations ? 1 : 0);
+}
+
+int kge_ship_step(const kge_model_desc* m, int32_t mode, const kge_ship_desc* sh, int32_t stage,
+                  const kge_adam_desc* adam, float* grad_entity, float* grad_relation, float* grad_modulus,
+                  float* losses_out, void* workspace, size_t workspace_bytes, int32_t* err_flag, void* stream) {
+  Geom geo;
+  int st = check_model(m, &geo);
+  if (st) return st;
+  if (mode != KGE_HEAD_BATCH && mode != KGE_TAIL_BATCH) return KGE_ERR_MODE;
+  if (!sh || stage < KGE_SHIP_Q || stage > KGE_SHIP_ENTITY || !err_flag) return KGE_ERR_ARG;
+  const int64_t B = sh->batch, n = sh->nneg;
+  if (!sh->pos || !sh->neg || B < 1 || n < 1 || n > 8192) return KGE_ERR_ARG;
+  if (sh->world < 1 || sh->world > 4096 || sh->rank < 0 || sh->rank >= sh->world) return KGE_ERR_ARG;
+  if (sh->own_begin < 0 || sh->own_end < sh->own_begin || sh->own_end > m->nentity) return KGE_ERR_ARG;
+  if (!sh->uni_weight && (!sh->subsampling_weight || !sh->weight_sum)) return KGE_ERR_ARG;
+  const bool head = (mode == KGE_HEAD_BATCH);
+  if (!sh->q || !sh->part || !sh->parts || !sh->scores || !sh->g || !sh->dq || !sh->pstats || !sh->ent_contrib ||
+      !sh->rel_contrib || !sh->row_stats || (head && (!sh->qp || !sh->pq)))
+    return KGE_ERR_ARG;
+  if (stage >= KGE_SHIP_CHAIN && !grad_relation) return KGE_ERR_ARG;
+  if (stage == KGE_SHIP_ENTITY && (!grad_entity || !losses_out || (m->model == KGE_PROTATE && !grad_modulus)))
+    return KGE_ERR_ARG;
+  if (adam && (!adam->entity.param || !adam->entity.exp_avg || !adam->entity.exp_avg_sq ||
+               adam->entity.param != m->entity_embedding))
+    return KGE_ERR_ARG;
+  size_t need = 0;
+  GradWs w = carve_grad(workspace, m, B, n, &need);
+  if (!workspace || workspace_bytes < need) return KGE_ERR_WORKSPACE;
+  hipStream_t s = as_stream(stream);
+  const ModelOps& op = ops_for(m->model);
+  const int kmode = head ? HEAD_BATCH : TAIL_BATCH;
+  const int Le = m->entity_dim, Lr = m->relation_dim;
+
+  RowArgs ra = row_args(m, geo, sh->pos, sh->neg, n, B, n, w, err_flag);
+  ra.op = ROW_TRAIN;
+  ra.adversarial = sh->adversarial ? 1 : 0;
+  ra.adv_T = sh->adversarial_temperature;
+  ra.uni_weight = sh->uni_weight ? 1 : 0;
+  ra.uni_inv = 1.f / (float)(sh->uni_batch > 0 ? sh->uni_batch : B);
+  ra.sub_w = sh->subsampling_weight;
+  ra.w_sum = sh->weight_sum;
+  ra.q_out = sh->q; ra.dq_out = sh->dq; ra.g_out = sh->g;
+  ra.ent_contrib = sh->ent_contrib; ra.rel_contrib = sh->rel_contrib; ra.row_stats = sh->row_stats;
+  ra.n_lds = 0; ra.fuse_epi = 0;
+  ra.sh.own_lo = sh->own_begin; ra.sh.own_hi = sh->own_end;
+  ra.sh.world = sh->world; ra.sh.me = sh->rank;
+  ra.sh.q_in = sh->q; ra.sh.qp_in = sh->qp; ra.sh.qp_out = sh->qp;
+  ra.sh.part_out = sh->part; ra.sh.parts_in = sh->parts; ra.sh.s_out = sh->scores;
+  ra.sh.pq = sh->pq; ra.sh.pstats = sh->pstats;
+  Side* sd = side_for_device();
+
+  if (stage == KGE_SHIP_Q) return launch_status(op.row(kmode, geo.vec, geo.ns, 3, ra, 0, s));
+  if (stage == KGE_SHIP_ROWS) {
+    // the occurrence CSR of the global batch beside the row pass (it needs only the ids)
+    CsrArgs ca;
+    ca.pos = sh->pos; ca.neg = sh->neg; ca.neg_stride = n;
+    ca.B = B; ca.n = n; ca.Bn = B * n; ca.E = m->nentity; ca.R = m->nrelation;
+    ca.keys = w.keys; ca.cnt = w.cnt; ca.off = w.off; ca.tmp = w.tmp; ca.occ = w.occ; ca.err = err_flag;
+    ca.scan_tmp = w.scan_tmp; ca.scan_tmp_bytes = w.scan_tmp_bytes;
+    hipStream_t ss = sd ? sd->s : s;
+    if (sd) {
+      hipEventRecord(sd->fork, s);
+      hipStreamWaitEvent(ss, sd->fork, 0);
+    }
+    st = launch_status(launch_csr(ca, ss));
+    if (st) return st;
+    if (sd) hipEventRecord(sd->csr_done, ss);
+    const size_t lds = sizeof(float) * (2 * 64 * (size_t)geo.ns * geo.vec + (size_t)vb_floats(Le) + 32);
+    if (lds > 64 * 1024) return KGE_ERR_DIM;
+    return launch_status(op.row(kmode, geo.vec, geo.ns, 4, ra, lds, s));
+  }
+  if (stage == KGE_SHIP_MERGE) return launch_status(op.row(kmode, geo.vec, geo.ns, 5, ra, 0, s));
+
+  const int nsl = entity_slices(geo, B, Le);
+  const int64_t ent_parts = m->nentity * (int64_t)(nsl > 0 ? nsl : 1);
+  const float reg = sh->regularization;
+  if (stage == KGE_SHIP_CHAIN) {
+    st = launch_status(op.row(kmode, geo.vec, geo.ns, 6, ra, 0, s));
+    if (st) return st;
+    if (sd) hipStreamWaitEvent(s, sd->csr_done, 0);  // the relation pass reads the CSR
+    RelArgs rl;
+    memset(&rl, 0, sizeof(rl));
+    rl.rel = m->relation_embedding; rl.R = m->nrelation; rl.E = m->nentity; rl.B = B; rl.Bn = B * n; rl.Lr = Lr;
+    rl.off = w.off; rl.occ = w.occ; rl.rel_contrib = sh->rel_contrib;
+    rl.reg3 = (sh->rank == 0) ? 3.f * reg : 0.f;  // the relation table is replicated: its regulariser once
+    rl.reg_partial = w.reg_partial + ent_parts; rl.grad_rel = grad_relation;
+    rl.write_grad = 1;
+    return launch_status(launch_rel_rows(rl, s));
+  }
+
+  // KGE_SHIP_ENTITY
+  AdamK ak;
+  ak.b1 = adam ? adam->beta1 : 0.f;
+  ak.b2 = adam ? adam->beta2 : 0.f;
+  ak.eps = adam ? adam->eps : 0.f;
+  auto adam_t = [&](const kge_adam_tensor* t) {
+    AdamT o;
+    o.p = (adam && t && t->param) ? t->param : nullptr;
+    o.m = o.p ? t->exp_avg : nullptr;
+    o.v = o.p ? t->exp_avg_sq : nullptr;
+    o.step_size = o.p ? t->step_size : 0.f;
+    o.bc2s = o.p ? t->bias_correction2_sqrt : 1.f;
+    return o;
+  };
+  EntArgs ea;
+  memset(&ea, 0, sizeof(ea));
+  ea.ent = m->entity_embedding; ea.modulus = m->modulus; ea.E = m->nentity; ea.Le = Le; ea.eg = geo.eg;
+  ea.e_begin = sh->own_begin; ea.e_end = sh->own_end;
+  ea.c = consts_of(m); ea.off = w.off; ea.occ = w.occ; ea.Bn = B * n; ea.n = n;
+  ea.g = sh->g; ea.q = sh->q; ea.ent_contrib = sh->ent_contrib; ea.reg3 = 3.f * reg; ea.reg_partial = w.reg_partial;
+  ea.grad_ent = grad_entity;
+  ea.write_grad = (!adam || adam->write_grad) ? 1 : 0;
+  ea.nsl = nsl;
+  ea.slice_w = nsl > 0 ? (geo.eg.S + nsl - 1) / nsl : 0;
+  ea.adam = adam_t(adam ? &adam->entity : nullptr);
+  ea.adamk = ak;
+  ea.B = B;
+  ea.rel_blocks = 0;
+  if (sh->own_end > sh->own_begin) {
+    st = launch_status(op.entity(kmode, geo.vec, geo.ns, ea, s));
+    if (st) return st;
+  }
+  FinArgs fa;
+  memset(&fa, 0, sizeof(fa));
+  fa.row_stats = sh->row_stats;
+  fa.sub_w = sh->subsampling_weight;
+  fa.w_sum = sh->weight_sum;
+  fa.B = B;
+  fa.uni_weight = sh->uni_weight ? 1 : 0;
+  fa.uni_n = (float)(sh->uni_batch > 0 ? sh->uni_batch : B);
+  fa.losses = losses_out;
+  fa.err = err_flag;
+  fa.reg_partial = (reg != 0.f) ? w.reg_partial : nullptr;
+  const int64_t per = nsl > 0 ? nsl : 1;
+  fa.reg_a0 = sh->own_begin * per;
+  fa.reg_a1 = sh->own_end * per;
+  fa.reg_b0 = ent_parts;
+  fa.reg_b1 = ent_parts + (sh->rank == 0 ? m->nrelation : 0);
+  fa.regularization = reg;
+  fa.grad_modulus = (m->model == KGE_PROTATE) ? grad_modulus : nullptr;
+  fa.adam = adam_t((adam && m->model == KGE_PROTATE) ? &adam->modulus : nullptr);
+  fa.adamk = ak;
+  return launch_status(launch_finalize(fa, s));
 }
 
 int kge_train_csr(const kge_model_desc* m, int32_t mode, const int64_t* pos, const int64_t* neg, int64_t batch,

@@ -12,6 +12,23 @@ namespace kge {
 
 enum RowOp : int { ROW_TRAIN = 0, ROW_GIVEN = 1 };
 
+// Query shipping (kge_ship_step): this rank holds only the entity rows
+// [own_lo, own_hi) of the table; the row kernels see the GLOBAL batch and
+// the shipped q vectors, and touch only owned rows (the table pointer is the
+// shard's base minus own_lo rows, so rows keep their global ids).
+struct ShipArgs {
+  int64_t own_lo, own_hi;
+  int world, me;
+  const float* q_in;      // [B, Le] q of every row (summed over the shards)
+  const float* qp_in;     // [B, Le] head-batch: the positive's tail-form q (h∘r)
+  float* qp_out;          // k_ship_q, head-batch
+  float* part_out;        // [B, 4] this shard's (max T·s, Z, NL, MG) per row
+  const float* parts_in;  // [world, B, 4] every shard's
+  float* s_out;           // [B, n] raw scores of the owned negatives
+  float* pq;              // [B, Le] head-batch: dL/d(h∘r) of the positive
+  float* pstats;          // [B, 4] positive statistics (owner of t; zero elsewhere)
+};
+
 struct ScoreArgs {
   const float* ent;
   const float* rel;
@@ -58,6 +75,7 @@ struct RowArgs {
   int fuse_epi;       // 1: k_row runs the epilogue in its tail, no k_row_epi launch
   int32_t* err;
   void (*timer_mid)(hipStream_t);  // stage-timer hook between the row-pass launches (or null)
+  ShipArgs sh;        // query shipping stages only
 };
 
 // k_row's LDS merge buffer: [2][Le] floats, and at least the 256 floats the

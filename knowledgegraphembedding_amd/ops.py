@@ -339,6 +339,23 @@ def train_step_from_rows(desc: _lib.ModelDesc, mode: str, pos: torch.Tensor, neg
     _lib.check(getattr(_lib.load(), fn)(*args), fn)
 
 
+def ship_step(desc: _lib.ModelDesc, mode: str, stage: int, ship: _lib.ShipDesc, dev, *,
+              adam: Optional[_lib.AdamDesc] = None, grad_entity_ptr: int = 0,
+              grad_relation: Optional[torch.Tensor] = None, grad_modulus: Optional[torch.Tensor] = None,
+              losses: Optional[torch.Tensor] = None, workspace: Optional[torch.Tensor] = None) -> None:
+    """One stage of the query-shipping step (kge_ship_step; partition.py
+    exchange "queries" drives the stages and the collectives between them).
+    `desc` and `grad_entity_ptr` address the shard by GLOBAL row id (base
+    pointers own_begin rows before the shard)."""
+    if mode not in ("head-batch", "tail-batch"):
+        raise ValueError("Training batch mode %s not supported" % mode)
+    ws = workspace if workspace is not None else _train_ws(desc, ship.batch, ship.nneg, dev)
+    st = state(dev)
+    _lib.check(_lib.load().kge_ship_step(desc, _lib.MODE_IDS[mode], ship, int(stage), adam, grad_entity_ptr or None,
+                                         _ptr(grad_relation), _ptr(grad_modulus), _ptr(losses), ws.data_ptr(),
+                                         ws.numel(), st.err.data_ptr(), _stream(dev)), "kge_ship_step")
+
+
 def adam_step(param: torch.Tensor, grad: torch.Tensor, exp_avg: torch.Tensor, exp_avg_sq: torch.Tensor, *,
               step: int, lr: float, beta1: float, beta2: float, eps: float) -> None:
     """torch.optim.Adam's update for one tensor (bias corrections in double, like torch)."""

@@ -40,6 +40,26 @@ reduce-scatter + all-gather — and the occurrence work of one single-GPU
 entity pass; the rows' gradients, the Adam update and the relation pass are
 bit-identical to one process training on the global batch.
 
+Exchange "queries" (query shipping): no replica at all — each
+rank holds only its shard (and its Adam moments), so the table's memory is
+split world ways.  The ranks ship the global batch's ids and q vectors
+instead of rows (kge_ship_step; the stages and collectives in _ship_step):
+
+  all-gather ids/weights → q from the owner of its row, all-reduce(q)
+  → every shard scores the negatives it owns for every row (partial softmax
+  state, V) → all-gather the per-row states (16 B per row and shard)
+  → merge in shard order; dL/dq shares, dL/ds, the positive on the owner of t
+  → all-reduce(dL/dq) → chain rule on the owners of h / t; the relation
+  gradient all-reduced → entity pass + fused Adam of the owned rows.
+
+Per rank and step that is ≈ 2·B·d_e·4 bytes (q out, dL/dq back) plus the
+ids instead of (N−1)/N of the table (see DESIGN §9 for the byte model).  The
+cross-shard sums (softmax normaliser, dL/dq, relation gradient) run in
+shard order, so the result matches one process to fp32 rounding, not bit
+for bit.  ``model.entity_embedding`` is an empty placeholder while training;
+``materialize()`` (collective) gathers the table for test_step / save_model
+and ``release()`` drops it again.
+
 Checkpoints stay in the reference layout: ``gathered_optimizer_state_dict``
 rebuilds the Adam state of the full table, ``load_optimizer_state_dict``
 slices a full-table state back to the shard.
@@ -48,6 +68,7 @@ from __future__ import annotations
 
 import copy
 import os
+from argparse import Namespace
 
 import torch
 import torch.distributed as dist
@@ -76,8 +97,8 @@ class EntityRowPartition:
     """
 
     def __init__(self, model, group=None, exchange: str = "grads"):
-        if exchange not in ("grads", "factors"):
-            raise ValueError(f"row-partition exchange must be grads or factors, not {exchange!r}")
+        if exchange not in ("grads", "factors", "queries"):
+            raise ValueError(f"row-partition exchange must be grads, factors or queries, not {exchange!r}")
         self.exchange = exchange
         self.group = group
         self.world = dist.get_world_size(group)
@@ -88,7 +109,27 @@ class EntityRowPartition:
         self.rows = -(-E // self.world)
         self.lo = self.rank * self.rows
         self.hi = min(E, self.lo + self.rows)
+        self.nown = max(0, self.hi - self.lo)  # the last shards may be short (or empty)
         dev = ent.device
+        self._pending = []  # (all-gather work, staging buffer, shard rows c0, c1) of the owner step's chunks
+        self._stage = {}
+        self.model = model
+        model.row_partition = self
+        if exchange == "queries":
+            self.shard = nn.Parameter(torch.zeros(self.rows, d, device=dev), requires_grad=ent.requires_grad)
+            with torch.no_grad():
+                self.shard[:self.nown].copy_(ent.detach()[self.lo:self.lo + self.nown])
+            self.full = self.grad_full = None
+            self.grad_shard = torch.zeros(self.rows, d, device=dev)
+            self._ship = None
+            self._placeholder = nn.Parameter(torch.empty(0, d, device=dev), requires_grad=ent.requires_grad)
+            model.entity_embedding = self._placeholder  # the whole table is never held during training
+            rel = model.relation_embedding
+            gm = torch.empty(1, 1, device=dev) if model.model_name == 'pRotatE' else None
+            model._grad_bufs = (torch.empty(0, d, device=dev),  # the placeholder's shape; the shard's is grad_shard
+                                torch.empty_like(rel, memory_format=torch.contiguous_format), gm,
+                                torch.empty(5, device=dev))
+            return
         self.full = torch.zeros(self.world * self.rows, d, device=dev)
         self.full[:E].copy_(ent.detach())
         if exchange == "factors":  # the owner updates its rows of the replica in place
@@ -105,10 +146,6 @@ class EntityRowPartition:
                             torch.empty(5, device=dev))
         if exchange == "grads":
             model.fuse_optimizer = False  # Adam runs on the shard, not on the replica the kernel reads
-        model.row_partition = self
-        self.model = model
-        self._pending = []  # (all-gather work, staging buffer, shard rows c0, c1) of the owner step's chunks
-        self._stage = {}
 
     # ------------------------------------------------------------ parameters
     def parameters(self):
@@ -122,7 +159,10 @@ class EntityRowPartition:
     def gather(self) -> None:
         """Refresh the replica from every rank's shard (all-gather).  After an
         owner step whose chunks were already put on the wire
-        (_owner_step), wait for those and place them instead."""
+        (_owner_step), wait for those and place them instead.  Query
+        shipping keeps no replica: nothing to do."""
+        if self.exchange == "queries":
+            return
         if self._pending:
             for work, stage, c0, c1 in self._pending:
                 work.wait()
@@ -139,7 +179,26 @@ class EntityRowPartition:
     def reload_from_replica(self) -> None:
         """After writing the replica (load_state_dict), take this rank's rows back."""
         with torch.no_grad():
+            if self.exchange == "queries":
+                self.shard[:self.nown].copy_(self.model.entity_embedding.detach()[self.lo:self.lo + self.nown])
+                return
             self.shard.copy_(self.full[self.lo:self.lo + self.rows])
+
+    def materialize(self) -> torch.Tensor:
+        """Query shipping: gather every rank's shard into a full table and make
+        it ``model.entity_embedding`` (for test_step / save_model / loading a
+        checkpoint; collective).  Other exchanges: the replica, as is."""
+        if self.exchange != "queries":
+            return self.model.entity_embedding
+        full = torch.empty(self.world * self.rows, self.dim, device=self.shard.device)
+        dist.all_gather_into_tensor(full, self.shard.detach(), group=self.group)
+        self.model.entity_embedding = nn.Parameter(full[:self.nentity], requires_grad=self._placeholder.requires_grad)
+        return self.model.entity_embedding
+
+    def release(self) -> None:
+        """Query shipping: drop the gathered table again (training needs only the shard)."""
+        if self.exchange == "queries":
+            self.model.entity_embedding = self._placeholder
 
     # -------------------------------------------------------------- training
     def train_grads(self, model, positive_sample, negative_sample, subsampling_weight, mode, args, optimizer=None):
@@ -149,6 +208,9 @@ class EntityRowPartition:
         if self.exchange == "factors":
             return self._owner_step(model, positive_sample, negative_sample, subsampling_weight, mode, args,
                                     optimizer)
+        if self.exchange == "queries":
+            return self._ship_step(model, positive_sample, negative_sample, subsampling_weight, mode, args,
+                                   optimizer)
         group = self.group
         B = positive_sample.shape[0]
         wsum = None if args.uni_weight else dp_weight_sum(subsampling_weight, group)
@@ -210,6 +272,113 @@ class EntityRowPartition:
             model.modulus.grad = gm
         if args.regularization != 0.0:  # each rank summed |x|^3 over its rows only
             dist.all_reduce(losses[3:4], op=dist.ReduceOp.SUM, group=self.group)
+            losses[2] = (losses[0] + losses[1]) / 2 + losses[3]
+        return losses
+
+    def _ship_buffers(self, model, Bg: int, n: int):
+        """Per-step buffers of the query-shipping step, reused while the shape holds."""
+        key = (Bg, n)
+        if self._ship is not None and self._ship[0] == key:
+            return self._ship[1]
+        dev, Le, Lr = self.shard.device, self.dim, model.relation_embedding.shape[1]
+        f32 = dict(device=dev, dtype=torch.float32)
+        b = Namespace(
+            pos=torch.empty(Bg, 3, dtype=torch.int64, device=dev), neg=torch.empty(Bg, n, dtype=torch.int64, device=dev),
+            w=torch.empty(Bg, **f32),
+            qq=torch.empty(2 * Bg * Le, **f32),                # q | qp (head-batch)
+            part=torch.empty(Bg, 4, **f32), parts=torch.empty(self.world * Bg, 4, **f32),
+            scores=torch.empty(Bg, n, **f32), g=torch.empty(Bg, n, **f32),
+            flat=torch.empty(Bg * Le + 4 * Bg + Bg * Le, **f32),  # dq | pstats | pq (head-batch)
+            ent_contrib=torch.empty(2 * Bg, Le, **f32), rel_contrib=torch.empty(Bg, Lr, **f32),
+            row_stats=torch.empty(Bg, 4, **f32))
+        self._ship = (key, b)
+        return b
+
+    def _ship_model_desc(self, model):
+        """The model descriptor for the shard: entity rows addressed by global id."""
+        from . import ops
+        g, rng = model._host_scalars()
+        d = ops.make_desc(model.model_name, self.shard.detach(), model.relation_embedding.detach(), g, rng,
+                          None if model._modulus() is None else model._modulus().detach())
+        d.entity_embedding = self.shard.data_ptr() - self.lo * self.dim * 4
+        d.nentity = self.nentity
+        return d
+
+    def _ship_step(self, model, positive_sample, negative_sample, subsampling_weight, mode, args, optimizer):
+        from . import ops
+        group, dev = self.group, self.shard.device
+        B, n = negative_sample.shape
+        Bg, Le = B * self.world, self.dim
+        head = mode == 'head-batch'
+        b = self._ship_buffers(model, Bg, n)
+        # the global batch, rank order (what one process would train on)
+        dist.all_gather_into_tensor(b.pos, positive_sample.to(dev, torch.int64).contiguous(), group=group)
+        dist.all_gather_into_tensor(b.neg, negative_sample.to(dev, torch.int64).contiguous(), group=group)
+        uni = bool(args.uni_weight)
+        wsum = None
+        if not uni:
+            dist.all_gather_into_tensor(b.w, subsampling_weight.to(dev, torch.float32).contiguous().view(-1),
+                                        group=group)
+            wsum = dp_weight_sum(subsampling_weight, group)
+        row_bytes = self.dim * 4
+        adam = None
+        if optimizer is not None and model.fuse_optimizer and hasattr(optimizer, 'prepare_fused'):
+            adam = optimizer.prepare_fused(self.shard, model.relation_embedding, model._modulus(),
+                                           write_grad=model.keep_grads)
+            if adam is not None:  # entity pointers by global row id, like the descriptor's
+                off = self.lo * row_bytes
+                adam.entity.param -= off
+                adam.entity.exp_avg -= off
+                adam.entity.exp_avg_sq -= off
+        _, gr, gm, losses = model._grad_buffers()
+        sd = _lib.ShipDesc()
+        sd.world, sd.rank = self.world, self.rank
+        sd.own_begin = min(self.lo, self.nentity)
+        sd.own_end = sd.own_begin + self.nown
+        sd.pos, sd.neg, sd.batch, sd.nneg = b.pos.data_ptr(), b.neg.data_ptr(), Bg, n
+        sd.subsampling_weight = b.w.data_ptr()
+        sd.weight_sum = wsum.data_ptr() if wsum is not None else None
+        sd.uni_weight, sd.adversarial, sd.uni_batch = int(uni), int(bool(args.negative_adversarial_sampling)), Bg
+        sd.adversarial_temperature = float(getattr(args, 'adversarial_temperature', 1.0))
+        sd.regularization = float(args.regularization)
+        q_n = Bg * Le
+        sd.q, sd.qp = b.qq.data_ptr(), b.qq[q_n:].data_ptr()
+        sd.part, sd.parts = b.part.data_ptr(), b.parts.data_ptr()
+        sd.scores, sd.g = b.scores.data_ptr(), b.g.data_ptr()
+        sd.dq, sd.pstats, sd.pq = b.flat.data_ptr(), b.flat[q_n:].data_ptr(), b.flat[q_n + 4 * Bg:].data_ptr()
+        sd.ent_contrib, sd.rel_contrib, sd.row_stats = (b.ent_contrib.data_ptr(), b.rel_contrib.data_ptr(),
+                                                        b.row_stats.data_ptr())
+        desc = self._ship_model_desc(model)
+        ws = ops._train_ws(desc, Bg, n, dev)
+
+        def run(stage, **kw):
+            ops.ship_step(desc, mode, stage, sd, dev, workspace=ws, **kw)
+
+        run(_lib.SHIP_Q)
+        dist.all_reduce(b.qq[:(2 if head else 1) * q_n], op=dist.ReduceOp.SUM, group=group)
+        run(_lib.SHIP_ROWS)
+        dist.all_gather_into_tensor(b.parts, b.part, group=group)
+        run(_lib.SHIP_MERGE)
+        dist.all_reduce(b.flat[:q_n + 4 * Bg + (q_n if head else 0)], op=dist.ReduceOp.SUM, group=group)
+        run(_lib.SHIP_CHAIN, grad_relation=gr)
+        dist.all_reduce(gr, op=dist.ReduceOp.SUM, group=group)
+        rel = model.relation_embedding
+        if adam is not None:  # the relation rows' Adam (marked fused by prepare_fused), on the summed gradient
+            st = optimizer.state[rel]
+            _lib.check(_lib.load().kge_adam_step(rel.data_ptr(), gr.data_ptr(), st['exp_avg'].data_ptr(),
+                                                 st['exp_avg_sq'].data_ptr(), rel.numel(), adam.beta1, adam.beta2,
+                                                 adam.eps, adam.relation.step_size,
+                                                 adam.relation.bias_correction2_sqrt, ops._stream(dev)),
+                       "kge_adam_step")
+        run(_lib.SHIP_ENTITY, adam=adam, grad_entity_ptr=self.grad_shard.data_ptr() - self.lo * row_bytes,
+            grad_relation=gr, grad_modulus=gm, losses=losses)
+        self.shard.grad = self.grad_shard if adam is None or model.keep_grads else None
+        if rel.requires_grad:
+            rel.grad = gr
+        if gm is not None and model.modulus.requires_grad:
+            model.modulus.grad = gm
+        if args.regularization != 0.0:  # each rank summed |x|^3 over its rows (relations: rank 0)
+            dist.all_reduce(losses[3:4], op=dist.ReduceOp.SUM, group=group)
             losses[2] = (losses[0] + losses[1]) / 2 + losses[3]
         return losses
 
