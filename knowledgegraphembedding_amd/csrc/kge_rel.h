@@ -23,7 +23,31 @@ __device__ __forceinline__ void rel_row_chunks(const RelArgs& a, int64_t rr, int
     for (int u = 0; u < U; ++u)
 #pragma unroll
       for (int e = 0; e < 4; ++e) acc[u][e] = 0.f;
-    for (int32_t p = b0; p < b1; ++p) {
+    int32_t p = b0;
+    if (v4) {
+      // four occurrences' rows in flight per iteration (a relation can have
+      // thousands of occurrences in a large global batch); the sums keep the
+      // ascending occurrence order, so the bits are those of the plain loop
+      for (; p + 4 <= b1; p += 4) {
+        float4 x[4][U];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const float4* src = reinterpret_cast<const float4*>(a.rel_contrib + (a.occ[p + t] - a.Bn - 2 * a.B) * a.Lr);
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            const int c = c0 + u * 64 + lane;
+            x[t][u] = (c < nchunk) ? src[c] : make_float4(0.f, 0.f, 0.f, 0.f);
+          }
+        }
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            acc[u][0] += x[t][u].x; acc[u][1] += x[t][u].y; acc[u][2] += x[t][u].z; acc[u][3] += x[t][u].w;
+          }
+      }
+    }
+    for (; p < b1; ++p) {
       const int64_t i = a.occ[p] - a.Bn - 2 * a.B;
       const float* src = a.rel_contrib + i * a.Lr;
 #pragma unroll
