@@ -81,7 +81,7 @@ __global__ __launch_bounds__(256) void k_rel_rows(RelArgs a) {
   const int lane = threadIdx.x & 63;
   const int64_t rr = (int64_t)blockIdx.x * 4 + wave_id();
   if (rr >= a.R) return;
-  rel_row_chunks<4>(a, rr, lane);
+  rel_row_chunks<4, true>(a, rr, lane);
 }
 
 // ------------------------------------------------------------ finalise

@@ -10,7 +10,10 @@ namespace kge {
 // order (+ 3λ r|r|), written densely; with a fused optimizer the Adam update
 // of the row is applied while the gradient is in registers.  Lanes own float4
 // chunks c = lane + 64u of the row (scalar tail when Lr % 4 != 0).
-template <int U>
+// P4: four occurrence rows in flight (the standalone k_rel_rows; the trailing
+// blocks of k_entity_sl keep one, so the entity pass's register budget is
+// not set by this path)
+template <int U, bool P4 = false>
 __device__ __forceinline__ void rel_row_chunks(const RelArgs& a, int64_t rr, int lane) {
   const int32_t b0 = a.off[a.E + rr], b1 = a.off[a.E + rr + 1];
   const float* row = a.rel + rr * a.Lr;
@@ -24,7 +27,7 @@ __device__ __forceinline__ void rel_row_chunks(const RelArgs& a, int64_t rr, int
 #pragma unroll
       for (int e = 0; e < 4; ++e) acc[u][e] = 0.f;
     int32_t p = b0;
-    if (v4) {
+    if (P4 && v4) {
       // four occurrences' rows in flight per iteration (a relation can have
       // thousands of occurrences in a large global batch); the sums keep the
       // ascending occurrence order, so the bits are those of the plain loop

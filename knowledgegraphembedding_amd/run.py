@@ -71,7 +71,8 @@ def parse_args(args=None):
     parser.add_argument('--nrelation', type=int, default=0, help='DO NOT MANUALLY SET')
     parser.add_argument('--row_partition', action='store_true',
                         help='multi-GPU only: each rank owns 1/world of the entity rows and their Adam state '
-                             '(reduce-scatter of gradients, all-gather of rows; partition.py)')
+                             '(partition.py; KGE_PART_EXCHANGE=factors|grads|queries, "queries" keeps only '
+                             'the shard on each rank and ships q vectors instead of rows)')
     parser.add_argument('--device_sampler', action='store_true',
                         help='build training batches on the GPU (sampler.py) instead of the CPU TrainDataset '
                              'workers: same sampling semantics, a different random stream')
@@ -271,6 +272,12 @@ def main(args):
         # collective under --row_partition: every rank calls it, rank 0 writes
         return part.gathered_optimizer_state_dict(optimizer) if part is not None else None
 
+    def full_table(on: bool) -> None:
+        # collective: query shipping keeps only shards; gather the whole table
+        # for checkpoints / evaluation and drop it again (other modes: no-op)
+        if part is not None:
+            part.materialize() if on else part.release()
+
     if args.do_train and getattr(args, 'device_sampler', False):
         from .sampler import DeviceTrainIterator
         train_iterator = DeviceTrainIterator(train_triples, nentity, nrelation, args.negative_sample_size,
@@ -289,9 +296,11 @@ def main(args):
         checkpoint = torch.load(os.path.join(args.init_checkpoint, 'checkpoint'), map_location='cpu',
                                 weights_only=True)
         init_step = checkpoint['step']
+        full_table(True)
         kge_model.load_state_dict(checkpoint['model_state_dict'])
         if part is not None:
             part.reload_from_replica()
+        full_table(False)
         if args.do_train:
             current_learning_rate = checkpoint['current_learning_rate']
             warm_up_steps = checkpoint['warm_up_steps']
@@ -327,23 +336,31 @@ def main(args):
                 warm_up_steps = warm_up_steps * 3
             if step % args.save_checkpoint_steps == 0:
                 osd = optimizer_state()
+                full_table(True)
                 if rank == 0:
                     save_model(kge_model, optimizer, {'step': step, 'current_learning_rate': current_learning_rate,
                                                       'warm_up_steps': warm_up_steps}, args, osd)
+                full_table(False)
             if step % args.log_steps == 0:
                 metrics = {}
                 for metric in training_logs[0].keys():
                     metrics[metric] = sum([log[metric] for log in training_logs]) / len(training_logs)
                 log_metrics('Training average', step, metrics)
                 training_logs = []
-            if args.do_valid and step % args.valid_steps == 0 and rank == 0:
-                logging.info('Evaluating on Valid Dataset...')
-                metrics = kge_model.test_step(kge_model, valid_triples, all_true_triples, args)
-                log_metrics('Valid', step, metrics)
+            if args.do_valid and step % args.valid_steps == 0:
+                full_table(True)
+                if rank == 0:
+                    logging.info('Evaluating on Valid Dataset...')
+                    metrics = kge_model.test_step(kge_model, valid_triples, all_true_triples, args)
+                    log_metrics('Valid', step, metrics)
+                full_table(False)
         osd = optimizer_state()
+        full_table(True)
         if rank == 0:
             save_model(kge_model, optimizer, {'step': step, 'current_learning_rate': current_learning_rate,
                                               'warm_up_steps': warm_up_steps}, args, osd)
+    else:
+        full_table(True)
 
     if rank != 0:
         return

@@ -103,3 +103,47 @@ def test_run_countries_config1_vs_reference_cli(tmp_path, golden_info):
     assert set(ckpt) == set(ref_ckpt)
     assert set(ckpt["model_state_dict"]) == set(ref_ckpt["model_state_dict"])
     assert ckpt["model_state_dict"]["entity_embedding"].shape == (271, 128)
+
+
+def _run_rowpart_worker(rank, world, port, data, save):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world), RANK=str(rank),
+                      LOCAL_RANK="0", KGE_PART_EXCHANGE="queries")
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.manual_seed(0)
+    args = run.parse_args(["--cuda", "--do_train", "--do_valid", "--do_test", "--device_sampler", "--row_partition",
+                           "--data_path", data, "--model", "RotatE", "-de", "-n", "16", "-b", "32", "-d", "16",
+                           "-g", "6.0", "-adv", "-lr", "0.01", "--max_steps", "30", "--valid_steps", "20",
+                           "--log_steps", "10", "--save_checkpoint_steps", "20", "--test_batch_size", "8",
+                           "-save", save, "-cpu", "1"])
+    run.main(args)
+    dist.destroy_process_group()
+
+
+def test_run_row_partition_query_shipping(tmp_path):
+    """--row_partition with KGE_PART_EXCHANGE=queries over 2 ranks (gloo, both
+    on cuda:0): each rank trains holding only its shard; checkpoints and the
+    valid/test passes gather the table (partition.materialize) — the saved
+    table has the full shape and a -init test pass reproduces rank 0's logged
+    test metrics."""
+    import socket
+    import torch.multiprocessing as mp
+    data, save = str(tmp_path / "data"), str(tmp_path / "save")
+    _dataset(data, E=41)  # an odd entity count: the second shard is one row short
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    mp.spawn(_run_rowpart_worker, args=(2, port, data, save), nprocs=2, join=True)
+    ckpt = torch.load(os.path.join(save, "checkpoint"), map_location="cpu", weights_only=True)
+    assert ckpt["step"] == 29
+    assert ckpt["model_state_dict"]["entity_embedding"].shape == (41, 32)
+    assert ckpt["optimizer_state_dict"]["state"][0]["exp_avg"].shape == (41, 32)
+    test1 = _metrics(os.path.join(save, "train.log"), "Test ")
+    assert set(test1) == {"MRR", "MR", "HITS@1", "HITS@3", "HITS@10"}
+    args2 = run.parse_args(["--cuda", "--do_test", "-init", save, "--test_batch_size", "8", "-cpu", "1"])
+    run.main(args2)
+    test2 = _metrics(os.path.join(save, "test.log"), "Test ")
+    for k in test1:
+        assert test2[k] == pytest.approx(test1[k], rel=0, abs=1e-12), k
