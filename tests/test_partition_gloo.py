@@ -138,3 +138,63 @@ def test_row_partition_matches_single_process(name, adv, uni, reg, world):
             np.testing.assert_allclose(got["positive_sample_loss"], ref[0], rtol=1e-5)
             np.testing.assert_allclose(got["negative_sample_loss"], ref[1], rtol=1e-5)
             np.testing.assert_allclose(got["loss"], ref[2], rtol=1e-5)
+
+
+def _ship_host_worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    model = _make_model("RotatE")
+    full = model.entity_embedding.detach().clone()
+    part = EntityRowPartition(model, exchange="queries")
+    res = {"placeholder": tuple(model.entity_embedding.shape), "shard": tuple(part.shard.shape),
+           "rows": (part.lo, part.lo + part.nown),
+           "shard_ok": bool(torch.equal(part.shard[:part.nown].detach(), full[part.lo:part.lo + part.nown]))}
+    with torch.no_grad():  # a step's worth of change on this rank's rows only
+        part.shard[:part.nown] += 1.0 + rank
+    table = part.materialize()
+    want = full.clone()
+    for r in range(world):
+        lo = r * part.rows
+        want[lo:min(E, lo + part.rows)] += 1.0 + r
+    res["gathered_ok"] = bool(torch.equal(table.detach(), want))
+    # a checkpoint written into the gathered table comes back to the shard
+    with torch.no_grad():
+        model.entity_embedding.mul_(2.0)
+    part.reload_from_replica()
+    res["reload_ok"] = bool(torch.equal(part.shard[:part.nown].detach(), 2.0 * want[part.lo:part.lo + part.nown]))
+    part.release()
+    res["released"] = tuple(model.entity_embedding.shape)
+    # optimizer state: shard moments gather to the full-table layout and slice back
+    opt = torch.optim.Adam(part.parameters(), lr=LR)
+    part.shard.grad = torch.ones_like(part.shard)
+    model.relation_embedding.grad = torch.zeros_like(model.relation_embedding)
+    opt.step()
+    sd = part.gathered_optimizer_state_dict(opt)
+    res["state_shape"] = tuple(sd["state"][0]["exp_avg"].shape)
+    opt2 = torch.optim.Adam(part.parameters(), lr=LR)
+    part.load_optimizer_state_dict(opt2, sd)
+    res["state_roundtrip"] = bool(torch.equal(opt2.state[part.shard]["exp_avg"][:part.nown],
+                                              opt.state[part.shard]["exp_avg"][:part.nown]))
+    out[rank] = res
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_query_shipping_shards_host(world):
+    """Query shipping's host side (partition.py exchange "queries") over gloo
+    on CPU: each rank keeps only its shard (the model's table becomes an
+    empty placeholder), materialize() gathers every rank's rows in order and
+    release() drops them, a checkpoint loaded into the gathered table reaches
+    the shard, and the shard's Adam state gathers to the reference's
+    full-table layout and slices back.  (The step itself runs only through
+    the HIP kernels: tests/test_ship_gpu.py.)"""
+    out = mp.Manager().dict()
+    mp.spawn(_ship_host_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    rows = -(-E // world)
+    for rank in range(world):
+        r = out[rank]
+        assert r["placeholder"] == (0, 2 * D) and r["released"] == (0, 2 * D)
+        assert r["shard"] == (rows, 2 * D)
+        assert r["rows"] == (rank * rows, min(E, (rank + 1) * rows))
+        assert r["shard_ok"] and r["gathered_ok"] and r["reload_ok"] and r["state_roundtrip"], r
+        assert r["state_shape"] == (E, 2 * D)
