@@ -674,7 +674,7 @@ int kge_ship_step(const kge_model_desc* m, int32_t mode, const kge_ship_desc* sh
   ra.w_sum = sh->weight_sum;
   ra.q_out = sh->q; ra.dq_out = sh->dq; ra.g_out = sh->g;
   ra.ent_contrib = sh->ent_contrib; ra.rel_contrib = sh->rel_contrib; ra.row_stats = sh->row_stats;
-  ra.n_lds = (int)(n + 4); ra.fuse_epi = 0;  // k_row<SH>: the per-wave lists of owned negatives
+  ra.n_lds = 0; ra.fuse_epi = 0;
   ra.sh.own_lo = sh->own_begin; ra.sh.own_hi = sh->own_end;
   ra.sh.world = sh->world; ra.sh.me = sh->rank;
   ra.sh.q_in = sh->q; ra.sh.qp_in = sh->qp; ra.sh.qp_out = sh->qp;
