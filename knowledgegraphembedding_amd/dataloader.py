@@ -151,11 +151,16 @@ class BidirectionalOneShotIterator(object):
 class RankShardSampler(torch.utils.data.Sampler):
     """Data-parallel training order: each epoch one permutation of the whole
     train set, drawn from a generator seeded by (seed, epoch) and therefore the
-    same on every rank, of which rank r takes positions r, r + world, ...  The
-    ranks' positives are disjoint within an epoch and together cover it; the
-    epoch advances on every new iteration (BidirectionalOneShotIterator
-    restarts the DataLoader endlessly), so no set_epoch call is needed.  With
-    world = 1 this is a plain reshuffle per epoch."""
+    same on every rank, of which rank r takes positions r, r + world, ... of
+    the first world·⌊n/world⌋.  Every rank's shard has the same length, so the
+    ranks' batches have the same size at every step (the factor / owner /
+    query-shipping exchanges all-gather per-row buffers of equal shape); the
+    n mod world left-over positions of an epoch's permutation — different
+    ones every epoch — wait for the next.  The ranks' positives are disjoint
+    within an epoch; the epoch advances on every new iteration
+    (BidirectionalOneShotIterator restarts the DataLoader endlessly), so no
+    set_epoch call is needed.  With world = 1 this is a plain reshuffle per
+    epoch."""
 
     def __init__(self, n: int, rank: int, world: int, seed: int):
         if world < 1 or not 0 <= rank < world:
@@ -164,10 +169,10 @@ class RankShardSampler(torch.utils.data.Sampler):
         self.epoch = 0
 
     def __len__(self):
-        return (self.n - self.rank + self.world - 1) // self.world
+        return self.n // self.world
 
     def __iter__(self):
         g = torch.Generator().manual_seed(self.seed * 1000003 + self.epoch)
         self.epoch += 1
         perm = torch.randperm(self.n, generator=g)
-        return iter(perm[self.rank::self.world].tolist())
+        return iter(perm[self.rank:self.world * len(self):self.world].tolist())
