@@ -239,6 +239,17 @@ int kge_train_step_from_rows(const kge_model_desc *m, int32_t mode, const int64_
  */
 int kge_train_csr(const kge_model_desc *m, int32_t mode, const int64_t *pos, const int64_t *neg, int64_t batch,
                   int64_t nneg, void *workspace, size_t workspace_bytes, int32_t *err_flag, void *stream);
+
+/*
+ * kge_train_csr for an owner of the entity rows [entity_begin, entity_end):
+ * only those entities' buckets are filled (the others stay empty; the
+ * relation buckets are all built) — what kge_train_step_from_rows_phased /
+ * _range with csr_ready read for that range, at 1/N of the fill and ordering
+ * work of the whole batch's CSR.
+ */
+int kge_train_csr_range(const kge_model_desc *m, int32_t mode, const int64_t *pos, const int64_t *neg,
+                        int64_t batch, int64_t nneg, int64_t entity_begin, int64_t entity_end, void *workspace,
+                        size_t workspace_bytes, int32_t *err_flag, void *stream);
 int kge_train_step_from_rows_csr(const kge_model_desc *m, int32_t mode, const int64_t *pos, const int64_t *neg,
                                  int64_t batch, int64_t nneg, const float *subsampling_weight,
                                  const float *weight_sum, int32_t uni_weight, int64_t uni_batch,

@@ -109,6 +109,7 @@ SIGNATURES = {
          _P, _SZ, _P, _P],
     ),
     "kge_train_csr": (C.c_int, [_DESC, _I32, _P, _P, _I64, _I64, _P, _SZ, _P, _P]),
+    "kge_train_csr_range": (C.c_int, [_DESC, _I32, _P, _P, _I64, _I64, _I64, _I64, _P, _SZ, _P, _P]),
     "kge_train_step_from_rows_range": (
         C.c_int,
         [_DESC, _I32, _P, _P, _I64, _I64, _P, _P, _I32, _I64, _F, _P, _P, _P, C.POINTER(AdamDesc), _P, _P, _P, _P,

@@ -222,7 +222,7 @@ int run_grad(const kge_model_desc* m, const Geom& geo, int mode, const int64_t* 
              int64_t neg_stride, int64_t B, int64_t n, RowArgs ra, GradWs w, float* grad_entity,
              float* grad_relation, float* grad_modulus, float reg, FinArgs fa, const kge_adam_desc* adam,
              int32_t* err, hipStream_t s, int phases = KGE_PHASE_ALL, int64_t e_begin = 0, int64_t e_end = -1,
-             int xstage = XS_NONE, int reg_relations = 1) {
+             int xstage = XS_NONE, int reg_relations = 1, int64_t csr_lo = 0, int64_t csr_hi = -1) {
   const ModelOps& op = ops_for(m->model);
   AdamK ak;
   ak.b1 = adam ? adam->beta1 : 0.f;
@@ -286,6 +286,7 @@ int run_grad(const kge_model_desc* m, const Geom& geo, int mode, const int64_t* 
   ca.pos = pos; ca.neg = neg; ca.neg_stride = neg_stride;
   ca.B = B; ca.n = n; ca.Bn = B * n; ca.E = m->nentity; ca.R = m->nrelation;
   ca.keys = w.keys; ca.cnt = w.cnt; ca.off = w.off; ca.tmp = w.tmp; ca.occ = w.occ; ca.err = err;
+  ca.e_lo = csr_lo; ca.e_hi = csr_hi < 0 ? m->nentity : csr_hi;
   ca.scan_tmp = w.scan_tmp; ca.scan_tmp_bytes = w.scan_tmp_bytes;
   if (xstage == XS_CSR_ONLY) return launch_status(launch_csr(ca, s));  // kge_train_csr
   if (from_rows) ra.fuse_epi = 0;  // the epilogue reads the gathered dL/dq (k_row_epi)
@@ -512,7 +513,7 @@ static int train_impl(const kge_model_desc* m, int32_t mode, const int64_t* pos,
                       float* losses_out, void* workspace, size_t workspace_bytes, int32_t* err_flag, void* stream,
                       int32_t phases = KGE_PHASE_ALL, int64_t e_begin = 0, int64_t e_end = -1, int xstage = XS_NONE,
                       float* rows_g = nullptr, float* rows_dq = nullptr, float* rows_stats = nullptr,
-                      int reg_relations = 1) {
+                      int reg_relations = 1, int64_t csr_lo = 0, int64_t csr_hi = -1) {
   Geom geo;
   int st = check_model(m, &geo);
   if (st) return st;
@@ -575,7 +576,7 @@ static int train_impl(const kge_model_desc* m, int32_t mode, const int64_t* pos,
   if (e_begin < 0 || e_begin > e_end || e_end > m->nentity) return KGE_ERR_ARG;
   return run_grad(m, geo, mode, pos, neg, nneg, batch, nneg, ra, w, grad_entity, grad_relation,
                   m->model == KGE_PROTATE ? grad_modulus : nullptr, regularization, fa, adam, err_flag, s, phases,
-                  e_begin, e_end, xstage, reg_relations);
+                  e_begin, e_end, xstage, reg_relations, csr_lo, csr_hi);
 }
 
 int kge_train_rows_slice(const kge_model_desc* m, int32_t mode, const int64_t* pos, const int64_t* neg,
@@ -689,6 +690,7 @@ int kge_ship_step(const kge_model_desc* m, int32_t mode, const kge_ship_desc* sh
     ca.pos = sh->pos; ca.neg = sh->neg; ca.neg_stride = n;
     ca.B = B; ca.n = n; ca.Bn = B * n; ca.E = m->nentity; ca.R = m->nrelation;
     ca.keys = w.keys; ca.cnt = w.cnt; ca.off = w.off; ca.tmp = w.tmp; ca.occ = w.occ; ca.err = err_flag;
+    ca.e_lo = sh->own_begin; ca.e_hi = sh->own_end;  // only this shard's rows are visited by its entity pass
     ca.scan_tmp = w.scan_tmp; ca.scan_tmp_bytes = w.scan_tmp_bytes;
     hipStream_t ss = sd ? sd->s : s;
     if (sd) {
@@ -780,6 +782,15 @@ int kge_train_csr(const kge_model_desc* m, int32_t mode, const int64_t* pos, con
                   int64_t nneg, void* workspace, size_t workspace_bytes, int32_t* err_flag, void* stream) {
   return train_impl(m, mode, pos, neg, batch, nneg, nullptr, nullptr, 1, 0, 1, 1.f, 0.f, nullptr, nullptr, nullptr,
                     nullptr, nullptr, workspace, workspace_bytes, err_flag, stream, KGE_PHASE_ALL, 0, -1, XS_CSR_ONLY);
+}
+
+int kge_train_csr_range(const kge_model_desc* m, int32_t mode, const int64_t* pos, const int64_t* neg,
+                        int64_t batch, int64_t nneg, int64_t entity_begin, int64_t entity_end, void* workspace,
+                        size_t workspace_bytes, int32_t* err_flag, void* stream) {
+  if (!m || entity_begin < 0 || entity_end < entity_begin || entity_end > m->nentity) return KGE_ERR_ARG;
+  return train_impl(m, mode, pos, neg, batch, nneg, nullptr, nullptr, 1, 0, 1, 1.f, 0.f, nullptr, nullptr, nullptr,
+                    nullptr, nullptr, workspace, workspace_bytes, err_flag, stream, KGE_PHASE_ALL, 0, -1, XS_CSR_ONLY,
+                    nullptr, nullptr, nullptr, 1, entity_begin, entity_end);
 }
 
 int kge_train_step_from_rows_csr(const kge_model_desc* m, int32_t mode, const int64_t* pos, const int64_t* neg,

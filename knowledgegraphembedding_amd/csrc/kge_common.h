@@ -15,6 +15,7 @@ struct CsrArgs {
   int32_t* tmp;   // [Bn + 3B]
   int32_t* occ;   // [Bn + 3B]
   int32_t* err;
+  int64_t e_lo, e_hi;  // entity buckets built: [e_lo, e_hi) (an owner's rows); the others stay empty
   void* scan_tmp;  // rocPRIM scan scratch (csr_scan_temp_bytes)
   size_t scan_tmp_bytes;
 };

@@ -36,6 +36,10 @@ __global__ __launch_bounds__(256) void k_csr_hist(CsrArgs a) {
       a.keys[k] = -1;
       continue;
     }
+    if (key < a.E && (key < a.e_lo || key >= a.e_hi)) {  // another owner's row: not bucketed here
+      a.keys[k] = -1;
+      continue;
+    }
     a.keys[k] = (int32_t)key;
     atomicAdd(&a.cnt[key], 1);
   }

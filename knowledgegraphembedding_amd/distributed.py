@@ -146,13 +146,15 @@ class RowFactors:
     __slots__ = ("pos", "neg", "w", "wsum", "g", "dq", "stats", "workspace", "B", "uni")
 
 
-def _exchange_row_factors(model, positive_sample, negative_sample, subsampling_weight, mode, args) -> RowFactors:
+def _exchange_row_factors(model, positive_sample, negative_sample, subsampling_weight, mode, args,
+                          csr_range=None) -> RowFactors:
     """Everything the factor-exchanging steps share: the global batch's ids and
     weights all-gathered, Σw over them, this rank's row pass into its place in
     the gather buffers (in FX_CHUNKS pieces, each piece's all-gather overlapping
     the next piece's row pass), the gathered dL/ds, dL/dq and row statistics,
     and the global batch's occurrence CSR built on a side stream as soon as the
-    ids arrive (FX_CSR_AHEAD, into `workspace`)."""
+    ids arrive (FX_CSR_AHEAD, into `workspace`; with `csr_range` (e0, e1)
+    only those entities' buckets — an owner's rows)."""
     from . import ops
     group = args.dp_group
     world = dist.get_world_size(group)
@@ -187,11 +189,11 @@ def _exchange_row_factors(model, positive_sample, negative_sample, subsampling_w
             with torch.cuda.stream(side):
                 for h in ids:
                     h.wait()
-                ops.train_csr(desc, mode, pos_g, neg_g, dev, workspace=gws)
+                ops.train_csr(desc, mode, pos_g, neg_g, dev, workspace=gws, entity_range=csr_range)
         else:
             for h in ids:
                 h.wait()
-            ops.train_csr(desc, mode, pos_g, neg_g, dev, workspace=gws)
+            ops.train_csr(desc, mode, pos_g, neg_g, dev, workspace=gws, entity_range=csr_range)
     Le = model.entity_dim
     g_g, dq_g, st_g = _fx_buffers(dev, Bg, n, Le)
     pieces = fx_pieces(B)

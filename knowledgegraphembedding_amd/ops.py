@@ -281,19 +281,27 @@ def train_rows_slice(desc: _lib.ModelDesc, mode: str, pos: torch.Tensor, neg: to
 
 
 def train_csr(desc: _lib.ModelDesc, mode: str, pos: torch.Tensor, neg: torch.Tensor, dev,
-              workspace: Optional[torch.Tensor] = None) -> None:
+              workspace: Optional[torch.Tensor] = None, entity_range: Optional[tuple] = None) -> None:
     """The occurrence CSR of the (gathered) batch into a step workspace
     (kge_train_csr), ahead of train_step_from_rows(..., csr_ready=True) with
     the SAME workspace — it needs only the ids, so it runs while the row
-    factors are on the wire."""
+    factors are on the wire.  With `entity_range` (e0, e1) only those
+    entities' buckets are built (kge_train_csr_range: an owner's rows)."""
     if mode not in ("head-batch", "tail-batch"):
         raise ValueError("Training batch mode %s not supported" % mode)
     pos, neg = _idx(pos, dev), _idx(neg, dev)
     B, n = neg.shape
     ws = workspace if workspace is not None else _train_ws(desc, B, n, dev)
     st = state(dev)
-    _lib.check(_lib.load().kge_train_csr(desc, _lib.MODE_IDS[mode], pos.data_ptr(), neg.data_ptr(), B, n,
-                                         ws.data_ptr(), ws.numel(), st.err.data_ptr(), _stream(dev)), "kge_train_csr")
+    lib = _lib.load()
+    if entity_range is not None:
+        e0, e1 = entity_range
+        _lib.check(lib.kge_train_csr_range(desc, _lib.MODE_IDS[mode], pos.data_ptr(), neg.data_ptr(), B, n, int(e0),
+                                           int(e1), ws.data_ptr(), ws.numel(), st.err.data_ptr(), _stream(dev)),
+                   "kge_train_csr_range")
+        return
+    _lib.check(lib.kge_train_csr(desc, _lib.MODE_IDS[mode], pos.data_ptr(), neg.data_ptr(), B, n,
+                                 ws.data_ptr(), ws.numel(), st.err.data_ptr(), _stream(dev)), "kge_train_csr")
 
 
 def train_step_from_rows(desc: _lib.ModelDesc, mode: str, pos: torch.Tensor, neg: torch.Tensor, sub_w: torch.Tensor,

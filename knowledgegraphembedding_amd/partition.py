@@ -234,7 +234,8 @@ class EntityRowPartition:
     def _owner_step(self, model, positive_sample, negative_sample, subsampling_weight, mode, args, optimizer):
         from . import ops
         dev = model.entity_embedding.device
-        fx = _dist._exchange_row_factors(model, positive_sample, negative_sample, subsampling_weight, mode, args)
+        fx = _dist._exchange_row_factors(model, positive_sample, negative_sample, subsampling_weight, mode, args,
+                                         csr_range=(min(self.lo, self.nentity), min(self.lo, self.nentity) + self.nown))
         adam = None
         if optimizer is not None and model.fuse_optimizer and hasattr(optimizer, 'prepare_fused_rows'):
             adam = optimizer.prepare_fused_rows(self.shard, model.entity_embedding, self.lo,

@@ -152,8 +152,9 @@ def _fx_worker(rank, world, port, uni, out):
         seen["slice"] = (uni_batch, None if wsum is None else float(wsum[0]))
         _fx_rows(pos, neg, w, g_out, dq_out, stats_out)
 
-    def csr(desc, mode, pos, neg, dev, workspace=None):
+    def csr(desc, mode, pos, neg, dev, workspace=None, entity_range=None):
         seen["csr"] = [t.clone() for t in (pos, neg)]
+        seen["csr_range"] = entity_range
 
     def from_rows(desc, mode, pos, neg, w, wsum, dev, *, uni_weight, uni_batch, regularization, g_in, dq_in, stats,
                   grad_entity, grad_relation, grad_modulus, losses, adam=None, csr_ready=False, workspace=None):
@@ -192,6 +193,7 @@ def test_factor_exchange_gathers_global_batch(uni, world):
         assert s["slice"][0] == B and s["global_scalars"][:2] == (B, 1e-3)
         # the CSR built ahead saw the same global ids the rest of the step sees
         assert s["csr_ready"] and all(torch.equal(a, b) for a, b in zip(s["csr"], s["global"][:2]))
+        assert s["csr_range"] is None  # every rank runs the whole global step: every entity's bucket
         if uni:
             assert s["slice"][1] is None and s["global_scalars"][2] is None
         else:  # Σw of the GLOBAL weights, on both sides of the exchange

@@ -107,8 +107,36 @@ def main():
                                      grad_relation=gr, grad_modulus=gm, losses=losses, adam=adam, csr_ready=True,
                                      entity_range=(0, rows_own), reg_relations=True)
             oopt.step()
-        ops.train_csr(desc, "tail-batch", pg, ng, dev)
+        ops.train_csr(desc, "tail-batch", pg, ng, dev, entity_range=(0, rows_own))
         res[f"owner_step_ms_N{world}_csr_ahead"] = timed(owner, a.reps)
+        res[f"csr_owner_range_ms_N{world}"] = timed(
+            lambda: ops.train_csr(desc, "tail-batch", pg, ng, dev, entity_range=(0, rows_own)), a.reps)
+
+        # one owner rank's whole device timeline without the collectives, as
+        # _exchange_row_factors + _owner_step issue it: the global CSR on a
+        # side stream beside the rank's row pass (FX_CHUNKS pieces), then the
+        # owner step — shows whether the CSR hides behind the row pass
+        side = torch.cuda.Stream(dev)
+        gws = ops.exchange_workspace(desc, Bg, N, dev)
+        pieces = [(0, B // 2), (B // 2, B)]
+
+        def rank_timeline():
+            side.wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.stream(side):
+                ops.train_csr(desc, "tail-batch", pg, ng, dev, workspace=gws, entity_range=(0, rows_own))
+            ops.weight_sum(wg, wsum)
+            for a0, a1 in pieces:
+                ops.train_rows_slice(desc, "tail-batch", pg[a0:a1], ng[a0:a1], wg[a0:a1], wsum, dev, adversarial=True,
+                                     temperature=1.0, uni_weight=False, uni_batch=Bg, g_out=g_g[a0:a1],
+                                     dq_out=dq_g[a0:a1], stats_out=st_g[a0:a1])
+            torch.cuda.current_stream(dev).wait_stream(side)
+            adam = oopt.prepare_fused_rows(shard, m.entity_embedding, 0, m.relation_embedding, None, write_grad=True)
+            ops.train_step_from_rows(desc, "tail-batch", pg, ng, wg, wsum, dev, uni_weight=False, uni_batch=Bg,
+                                     regularization=0.0, g_in=g_g, dq_in=dq_g, stats=st_g, grad_entity=ge,
+                                     grad_relation=gr, grad_modulus=gm, losses=losses, adam=adam, csr_ready=True,
+                                     entity_range=(0, rows_own), reg_relations=True, workspace=gws)
+            oopt.step()
+        res[f"owner_rank_compute_ms_N{world}"] = timed(rank_timeline, a.reps)
         res[f"owner_rows_allgather_bytes_in_N{world}"] = (world - 1) * rows_own * Le * 4
         res[f"csr_ms_N{world}"] = timed(lambda: ops.train_csr(desc, "tail-batch", pg, ng, dev), a.reps)
         res[f"exchange_bytes_per_rank_N{world}"] = (B * Le + B * N + 4 * B) * 4 + B * (N + 3) * 8 + 4 * B
