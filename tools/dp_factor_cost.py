@@ -19,7 +19,7 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from argparse import Namespace  # noqa: E402
 
-from knowledgegraphembedding_amd import KGEAdam, KGEModel, ops, synth  # noqa: E402
+from knowledgegraphembedding_amd import KGEAdam, KGEModel, _lib, ops, synth  # noqa: E402
 
 E, R, D, B, N = 14951, 1345, 1000, 1024, 256
 
@@ -120,7 +120,7 @@ def main():
         gws = ops.exchange_workspace(desc, Bg, N, dev)
         pieces = [(0, B // 2), (B // 2, B)]
 
-        def rank_timeline():
+        def rank_timeline(chunks=4):
             side.wait_stream(torch.cuda.current_stream(dev))
             with torch.cuda.stream(side):
                 ops.train_csr(desc, "tail-batch", pg, ng, dev, workspace=gws, entity_range=(0, rows_own))
@@ -129,14 +129,28 @@ def main():
                 ops.train_rows_slice(desc, "tail-batch", pg[a0:a1], ng[a0:a1], wg[a0:a1], wsum, dev, adversarial=True,
                                      temperature=1.0, uni_weight=False, uni_batch=Bg, g_out=g_g[a0:a1],
                                      dq_out=dq_g[a0:a1], stats_out=st_g[a0:a1])
-            torch.cuda.current_stream(dev).wait_stream(side)
             adam = oopt.prepare_fused_rows(shard, m.entity_embedding, 0, m.relation_embedding, None, write_grad=True)
-            ops.train_step_from_rows(desc, "tail-batch", pg, ng, wg, wsum, dev, uni_weight=False, uni_batch=Bg,
-                                     regularization=0.0, g_in=g_g, dq_in=dq_g, stats=st_g, grad_entity=ge,
-                                     grad_relation=gr, grad_modulus=gm, losses=losses, adam=adam, csr_ready=True,
-                                     entity_range=(0, rows_own), reg_relations=True, workspace=gws)
+            kw = dict(uni_weight=False, uni_batch=Bg, regularization=0.0, g_in=g_g, dq_in=dq_g, stats=st_g,
+                      grad_entity=ge, grad_relation=gr, grad_modulus=gm, losses=losses, adam=adam, csr_ready=True,
+                      reg_relations=True, workspace=gws)
+            if chunks <= 1:  # one call (the owner step's unchunked form)
+                torch.cuda.current_stream(dev).wait_stream(side)
+                ops.train_step_from_rows(desc, "tail-batch", pg, ng, wg, wsum, dev, entity_range=(0, rows_own), **kw)
+            else:  # as partition._owner_step: the CSR joined, ROWS, entity chunks, FINALIZE
+                torch.cuda.current_stream(dev).wait_stream(side)
+                ops.train_step_from_rows(desc, "tail-batch", pg, ng, wg, wsum, dev, entity_range=(0, rows_own),
+                                         phases=_lib.PHASE_ROWS, **kw)
+                step = -(-rows_own // chunks)
+                for c0 in range(0, rows_own, step):
+                    ops.train_step_from_rows(desc, "tail-batch", pg, ng, wg, wsum, dev,
+                                             entity_range=(c0, min(rows_own, c0 + step)), phases=_lib.PHASE_ENTITY,
+                                             **kw)
+                ops.train_step_from_rows(desc, "tail-batch", pg, ng, wg, wsum, dev, entity_range=(0, rows_own),
+                                         phases=_lib.PHASE_FINALIZE, **kw)
             oopt.step()
-        res[f"owner_rank_compute_ms_N{world}"] = timed(rank_timeline, a.reps)
+        res[f"owner_rank_compute_ms_N{world}_4chunks"] = timed(rank_timeline, a.reps)
+        res[f"owner_rank_compute_ms_N{world}_1chunk"] = timed(lambda: rank_timeline(1), a.reps)
+        res[f"owner_rank_compute_ms_N{world}_2chunks"] = timed(lambda: rank_timeline(2), a.reps)
         res[f"owner_rows_allgather_bytes_in_N{world}"] = (world - 1) * rows_own * Le * 4
         res[f"csr_ms_N{world}"] = timed(lambda: ops.train_csr(desc, "tail-batch", pg, ng, dev), a.reps)
         res[f"exchange_bytes_per_rank_N{world}"] = (B * Le + B * N + 4 * B) * 4 + B * (N + 3) * 8 + 4 * B
