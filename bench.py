@@ -217,7 +217,7 @@ def cpu_baseline(model_cpu_state, budget_s: float = 12.0, b: int = 32):
 
 def rank_section(dev, reps: int = 3) -> dict:
     """BASELINE config 3, measured live beside the training metric: filtered
-    ranking (KGEModel.rank_queries → kge_rank_filtered: MFMA tile + near-tie
+    ranking (KGEModel.rank_queries_both → kge_rank_filtered: MFMA tile + near-tie
     refinement in the reference's order) of all 3134 wn18rr-shape test triples
     in both directions (6268 queries, E=40943, d=500) against a synthetic
     filter graph of wn18rr's 93,003 true triples (tools/bench_rank.py, same
@@ -242,8 +242,7 @@ def rank_section(dev, reps: int = 3) -> dict:
         for rep in range(reps + 1):
             torch.cuda.synchronize()
             t0 = time.perf_counter()
-            rh, _ = m.rank_queries(test, index, "head-batch")
-            rt, _ = m.rank_queries(test, index, "tail-batch")
+            (rh, _), (rt, _) = m.rank_queries_both(test, index)
             torch.cuda.synchronize()
             dt = time.perf_counter() - t0
             if rep and (best is None or dt < best):

@@ -480,9 +480,11 @@ class KGEModel(nn.Module):
         row_bytes = max(4 * int(model.entity_dim), 4 * ((int(args.nentity) + 31) // 32))
         block = max(test_batch_size, min(16384, max(256, (128 << 20) // row_bytes)))
         step = 0
+        per_mode = []  # device rank tensors; read back once, after both directions are queued
         with torch.no_grad():
             for mode in ('head-batch', 'tail-batch'):
                 ranks_all = []
+                per_mode.append(ranks_all)
                 for b0 in range(0, len(triples), block):
                     q = triples[b0:b0 + block]
                     off, ids = index.filter_csr(q, mode)
@@ -495,9 +497,10 @@ class KGEModel(nn.Module):
                         if step % test_log_steps == 0:
                             logging.info('Evaluating the model... (%d/%d)' % (step, total_steps))
                         step += 1
+            for ranks_all in per_mode:  # head-batch, then tail-batch
                 ranks_np = torch.cat(ranks_all).cpu().numpy() if ranks_all else np.zeros(0, np.int64)
-                ops.raise_on_device_error(dev)
                 ranks_seq.extend(ranks_np.tolist())
+            ops.raise_on_device_error(dev)
         # model.py:405-427: per-query log entries averaged in order — the same
         # left-to-right float sums, without materialising a dict per query
         n = len(ranks_seq)
@@ -508,6 +511,25 @@ class KGEModel(nn.Module):
             'HITS@3': sum(1.0 if r <= 3 else 0.0 for r in ranks_seq) / n,
             'HITS@10': sum(1.0 if r <= 10 else 0.0 for r in ranks_seq) / n,
         }
+
+    def rank_queries_both(self, triples, all_true_triples, path="auto"):
+        """rank_queries for head-batch and tail-batch, both queued before the
+        one read-back (the tail direction's host filter CSR overlaps the head
+        direction's kernels, as in test_step).  Returns ((ranks, ties) head,
+        (ranks, ties) tail)."""
+        dev = ops._require_device(self.entity_embedding)
+        index = all_true_triples if isinstance(all_true_triples, FilterIndex) else \
+            FilterIndex(all_true_triples, self.nentity, self.nrelation)
+        q = np.asarray(triples, dtype=np.int64).reshape(-1, 3)
+        outs = []
+        with torch.no_grad():
+            for mode in ('head-batch', 'tail-batch'):
+                off, ids = index.filter_csr(q, mode)
+                outs.append(ops.rank_filtered(self.desc(), mode, torch.from_numpy(q), torch.from_numpy(off),
+                                              torch.from_numpy(ids), dev, path=path))
+        res = tuple(tuple(t.cpu().numpy() for t in out) for out in outs)
+        ops.raise_on_device_error(dev)
+        return res
 
     def rank_queries(self, triples, all_true_triples, mode, path="auto", listed=False):
         """Per-query filtered ranks and tie counts (numpy int64, int32) — the

@@ -88,3 +88,21 @@ def test_everything_filtered_ranks_first(name):
     true = np.array([[0, 1, t] for t in range(E)], dtype=np.int64)
     ranks, ties = m.rank_queries(true[:10], true, "tail-batch")
     assert np.array_equal(ranks, np.ones(10, dtype=np.int64)) and not ties.any()
+
+
+@pytest.mark.parametrize("name", ["DistMult", "RotatE"])
+def test_rank_queries_both_directions_pipelined(name):
+    """rank_queries_both (both directions queued, one read-back — what bench.py's
+    ranking section and test_step do) returns exactly rank_queries' per-direction
+    ranks and ties."""
+    E, R, d = 300, 5, 32
+    m, *_ = build_model(name, E, R, d, 12.0, 7)
+    rng = np.random.default_rng(3)
+    true = np.unique(np.stack([rng.integers(0, E, 2000), rng.integers(0, R, 2000), rng.integers(0, E, 2000)], 1),
+                     axis=0)
+    q = true[:257]
+    (rh, th), (rt, tt) = m.rank_queries_both(q, true)
+    rh1, th1 = m.rank_queries(q, true, "head-batch")
+    rt1, tt1 = m.rank_queries(q, true, "tail-batch")
+    assert np.array_equal(rh, rh1) and np.array_equal(th, th1)
+    assert np.array_equal(rt, rt1) and np.array_equal(tt, tt1)
