@@ -5,8 +5,10 @@ Against one process training on the whole batch the gradients, losses and
 tables agree to fp32 rounding (the softmax normaliser, dL/dq and the
 relation gradient are summed over the shards in shard order, so not bit
 for bit)."""
+import faulthandler
 import os
 import socket
+import sys
 from argparse import Namespace
 
 import numpy as np
@@ -53,6 +55,7 @@ def _args(group, reg, uni):
 
 
 def _worker(rank, world, port, name, reg, uni, e, d, env, out):
+    faulthandler.dump_traceback_later(45, repeat=True, file=sys.stderr)  # a slow rank shows where it waits
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), **env)
     torch.cuda.set_device(0)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -73,6 +76,7 @@ def _worker(rank, world, port, name, reg, uni, e, d, env, out):
                  "lo": part.lo, "hi": part.lo + part.nown,
                  "mod": model.modulus.detach().cpu().numpy() if name == "pRotatE" else None}
     dist.destroy_process_group()
+    faulthandler.cancel_dump_traceback_later()
 
 
 def _close(got, want, what, rtol=2e-4):
