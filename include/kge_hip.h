@@ -68,6 +68,13 @@ enum kge_status {
  *   phase_divisor_p = float(embedding_range.item() / 3.14159262358979323846)  model.py:232,236-238
  *                     (the reference's pi typo is part of the contract)
  *   modulus         = device pointer to the pRotatE [1,1] modulus (model.py:59-60), else NULL
+ *   relation_trig   = RotatE only, nullable: device [nrelation, 2, relation_dim] fp32 table of
+ *                     (cos θ | sin θ) of every relation phase θ = relation / phase_divisor, as
+ *                     the caller's reference evaluates them (model.py:209-212: the reference's
+ *                     ATen CPU cos / sin).  The filtered ranking (kge_rank_filtered*) then builds
+ *                     its queries' rotation from these values, so its ranks are the reference's
+ *                     bit for bit; NULL = correctly rounded cos / sin on the device.  Training
+ *                     and kge_score do not read it (scores are held to 1e-4, not to bits).
  */
 typedef struct kge_model_desc {
     int32_t model;
@@ -83,6 +90,7 @@ typedef struct kge_model_desc {
     const float *entity_embedding;   /* [nentity, entity_dim] */
     const float *relation_embedding; /* [nrelation, relation_dim] */
     const float *modulus;            /* [1] or NULL */
+    const float *relation_trig;      /* RotatE [nrelation, 2, relation_dim] or NULL (ranking only) */
 } kge_model_desc;
 
 /* Library identity (for the loader's symbol check). */
@@ -386,9 +394,12 @@ int kge_adam_step(float *param, const float *grad, float *exp_avg, float *exp_av
  * candidate whose score clears the true one's by more than a rounding bound
  * and lists the rest, which are re-scored in the reference's operation order
  * (the ATen elementwise ops and its sum(dim=2) / norm(p=1) reduction order) —
- * bit-exact to the reference for TransE, DistMult and ComplEx; RotatE and
- * pRotatE use correctly rounded cos/sin where the reference uses its CPU
- * vector library's (last-bit differences on a few percent of arguments).
+ * bit-exact to the reference for TransE, DistMult and ComplEx, and for RotatE
+ * when m->relation_trig holds the reference's cos / sin of the relation phases
+ * (without it: correctly rounded values, which differ from the reference's
+ * CPU vector library in the last bit on a few percent of arguments).
+ * pRotatE's sin acts on per-candidate phase sums, so it cannot be tabulated:
+ * correctly rounded there (ranks equal the reference's up to that last bit).
  */
 size_t kge_rank_workspace_bytes(const kge_model_desc *m, int64_t nq);
 int kge_rank_filtered(const kge_model_desc *m, int32_t mode, const int64_t *queries, int64_t nq,

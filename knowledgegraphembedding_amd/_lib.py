@@ -39,6 +39,7 @@ class ModelDesc(C.Structure):
         ("entity_embedding", C.c_void_p),
         ("relation_embedding", C.c_void_p),
         ("modulus", C.c_void_p),
+        ("relation_trig", C.c_void_p),
     ]
 
 

@@ -64,6 +64,36 @@ def _compile(hipcc: str, src: Path, obj: Path) -> tuple[Path, str]:
     return src, r.stderr
 
 
+TORCH_SRC = CSRC / "torch" / "kge_torch_ops.cpp"
+TORCH_LIB = PKG / "libkge_torch.so"
+
+
+def build_torch_ops(verbose: bool = False) -> Path:
+    """libkge_torch.so: the `kge` operator library (TORCH_LIBRARY, csrc/torch/),
+    host C++ against libtorch and libkge_hip.so — loaded by torch_ops.py with
+    torch.ops.load_library, or linked by a libtorch C++ caller."""
+    import torch
+    import torch.utils.cpp_extension as cx
+    deps = [TORCH_SRC, INCLUDE / "kge_hip.h", LIB]
+    if TORCH_LIB.exists() and all(p.stat().st_mtime <= TORCH_LIB.stat().st_mtime for p in deps):
+        return TORCH_LIB
+    tlib = cx.library_paths()[0]
+    cmd = [os.environ.get("CXX", "g++"), "-O2", "-std=c++17", "-fPIC", "-shared", "-Wall", "-Wno-unused-parameter",
+           "-Wno-return-type", f"-D_GLIBCXX_USE_CXX11_ABI={int(torch._C._GLIBCXX_USE_CXX11_ABI)}",
+           "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1", "-DTORCH_EXTENSION_NAME=kge_torch",
+           *[f"-I{p}" for p in cx.include_paths()], "-I/opt/rocm/include", f"-I{INCLUDE}",
+           str(TORCH_SRC), "-o", str(TORCH_LIB.with_suffix(".so.tmp")),
+           f"-L{tlib}", "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip", f"-Wl,-rpath,{tlib}",
+           f"-L{PKG}", "-lkge_hip", "-Wl,-rpath,$ORIGIN", "-L/opt/rocm/lib", "-lamdhip64"]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"libkge_torch.so build failed:\n{r.stdout}\n{r.stderr}")
+    if verbose and r.stderr.strip():
+        print(r.stderr, file=sys.stderr)
+    os.replace(TORCH_LIB.with_suffix(".so.tmp"), TORCH_LIB)
+    return TORCH_LIB
+
+
 def build(clean: bool = False, jobs: int | None = None, verbose: bool = False) -> Path:
     hipcc = _hipcc()
     if clean and BUILD.exists():
@@ -88,6 +118,9 @@ def build(clean: bool = False, jobs: int | None = None, verbose: bool = False) -
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{r.stdout}\n{r.stderr}")
         os.replace(tmp, LIB)
+    if clean and TORCH_LIB.exists():
+        TORCH_LIB.unlink()
+    build_torch_ops(verbose=verbose)
     return LIB
 
 

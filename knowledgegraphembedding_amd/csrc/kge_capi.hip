@@ -54,7 +54,7 @@ int check_model(const kge_model_desc* m, Geom* g) {
   const int S = span / g->vec;
   int ns = 1;
   while (64 * ns < S) ns *= 2;
-  if (ns > 8) return KGE_ERR_DIM;
+  if (ns > (g->vec == 4 ? 8 : 32)) return KGE_ERR_DIM;  // (half-)rows up to 2048 floats, any alignment
   g->ns = ns;
   g->eg.S = S;
   g->eg.half = g->cplx ? span : 0;
@@ -354,6 +354,11 @@ int run_grad(const kge_model_desc* m, const Geom& geo, int mode, const int64_t* 
   ea.rel_blocks = rel_fused ? (m->nrelation + 3) / 4 : 0;
   if (e_end > e_begin) {
     st = launch_status(op.entity(mode, geo.vec, geo.ns, ea, s));
+    if (st) return st;
+  } else if (rel_fused) {
+    // an owner with no entity rows (a trailing rank of a small table) still
+    // owes the relation pass the entity launch would have carried
+    st = launch_status(launch_rel_rows(rl, s));
     if (st) return st;
   }
   if (timed) g_timer.mark(s);
@@ -908,6 +913,9 @@ int kge_rank_filtered_ex(const kge_model_desc* m, int32_t mode, const int64_t* q
   if (nq > 65535) return KGE_ERR_DIM;  // the bitmap launch puts queries on grid.y
   const int rp = rank_path(m, path);
   if (rp < 0) return KGE_ERR_ARG;  // the requested fast pass cannot take these rows
+  // RotatE's reference cos | sin table (read with the row's slot geometry)
+  const float* trig = (m->model == KGE_ROTATE) ? m->relation_trig : nullptr;
+  if (trig && geo.vec == 4 && !aligned16(trig)) return KGE_ERR_ARG;
   size_t need = 0;
   RankWs w = carve_rank(workspace, m, nq, &need);
   if (!workspace || workspace_bytes < need) return KGE_ERR_WORKSPACE;
@@ -931,6 +939,7 @@ int kge_rank_filtered_ex(const kge_model_desc* m, int32_t mode, const int64_t* q
   a.q = w.q; a.s_true = w.s_true; a.true_id = w.true_id; a.gt = w.gt;
   a.fbits = w.bits; a.W = (m->nentity + 31) / 32; a.win = win; a.err = err_flag;
   a.prep_only = 1;
+  a.trig = trig;
   st = launch_status(ops.rank(mode, geo.vec, geo.ns, a, s));
   if (st) return st;
   // 2. excluded candidates (filtered ids + the true id) as a bitmap
@@ -962,6 +971,7 @@ int kge_rank_filtered_ex(const kge_model_desc* m, int32_t mode, const int64_t* q
   ra.exact_fast = (m->model == KGE_TRANSE && rp == RP_TILE) ? 1 : 0;
   ra.ucnt = w.ucnt; ra.ulist = w.ulist; ra.cap = RANK_CAP;
   ra.fbits = w.bits; ra.W = a.W; ra.gt = w.gt; ra.eq = w.eq; ra.gtx = w.gtx; ra.eqx = w.eqx; ra.err = err_flag;
+  ra.trig = trig;
   st = launch_status(ops.rank_ref(mode, 0, ra, s));
   if (st) return st;
   // 5. fast counting pass: clear cases counted, near-ties listed

@@ -265,6 +265,19 @@ template <int M, int MODE>
 struct Elem {
   static constexpr bool HEAD = (MODE == HEAD_BATCH);
 
+  // RotatE's rotation of x by (cos θ, sin θ) — the complex product of
+  // model.py:215-221, one IEEE op per ATen op.  Shared by the fast q and the
+  // reference-order q, so given the same cos / sin both have the same bits.
+  __device__ static __forceinline__ void rotate(float xa, float xb, float cs, float sn, float& qa, float& qb) {
+    if constexpr (HEAD) {                 // model.py:215-216
+      qa = cs * xa + sn * xb;
+      qb = cs * xb - sn * xa;
+    } else {                              // model.py:220-221
+      qa = xa * cs - xb * sn;
+      qb = xa * sn + xb * cs;
+    }
+  }
+
   __device__ static __forceinline__ void make_q(float xa, float xb, float ra, float rb, const Consts& c,
                                                 float& qa, float& qb) {
     if constexpr (M == TRANSE) {
@@ -286,14 +299,8 @@ struct Elem {
       const float th = ra / c.kappa;      // true fp32 division, model.py:209
       float sn, cs;
       sincosf(th, &sn, &cs);              // model.py:211-212
-      if constexpr (HEAD) {               // model.py:215-216
-        qa = cs * xa + sn * xb;
-        qb = cs * xb - sn * xa;
-      } else {                            // model.py:220-221
-        qa = xa * cs - xb * sn;
-        qb = xa * sn + xb * cs;
-      }
-    } else {                              // PROTATE, model.py:236-243
+      rotate(xa, xb, cs, sn, qa, qb);
+    } else {                            // PROTATE, model.py:236-243
       const float pr = ra / c.kappa_p;
       const float px = xa / c.kappa_p;
       qa = HEAD ? (pr - px) : (px + pr);

@@ -167,6 +167,7 @@ struct RankArgs {
   RankWin win;
   int32_t* err;
   int prep_only;        // launch k_rank_prep only (the MFMA / tile paths count on their own)
+  const float* trig;    // RotatE: [R, 2, Lr] reference cos | sin of the phases, or null
 };
 
 // Reference-order refinement (k_rank_window / k_rank_refine / k_rank_exact).
@@ -196,6 +197,7 @@ struct RefArgs {
   int32_t* gtx;            // overflowed queries: exact counts over every candidate
   int32_t* eqx;
   int32_t* err;
+  const float* trig;       // RotatE: [R, 2, Lr] reference cos | sin of the phases, or null
 };
 
 // Register-tiled filtered ranking (kge_kernels.inc, k_rank_tile): 64 queries ×

@@ -17,11 +17,14 @@
 //    RotatE and pRotatE;
 //  * `torch.norm(p=1, dim=2)` as a sequential fp32 sum for TransE.
 //
-// Every fp32 operation matches the reference bit for bit, except RotatE's
-// cos/sin and pRotatE's sin: the reference's vectorized CPU transcendentals
-// are not reproducible here; these use correctly rounded values (double
-// evaluation rounded once), which differ from the reference's in the last
-// bit for a few percent of arguments.
+// Every fp32 operation matches the reference bit for bit.  The reference's
+// vectorized CPU transcendentals cannot be reproduced on the device, so
+// RotatE's cos / sin of the relation phases come from a table the caller
+// evaluated with the reference's own ATen op (kge_model_desc.relation_trig);
+// without one — and always for pRotatE's sin of per-candidate phase sums —
+// correctly rounded values are used (double evaluation rounded once), which
+// differ from the reference's in the last bit on a few percent of arguments
+// (DESIGN.md §5).
 #pragma once
 #include "kge_device.h"
 
@@ -32,20 +35,24 @@ __device__ __forceinline__ float sin_rn(float x) { return (float)sin((double)x);
 __device__ __forceinline__ float cos_rn(float x) { return (float)cos((double)x); }
 __device__ __forceinline__ float sqrt_rn(float x) { return __fsqrt_rn(x); }
 
-// reference q for one element (model.py association; RotatE trig rounded once)
+// reference q for one element (model.py association).  RotatE: the rotation
+// (cos θ, sin θ) from the caller's table of the reference's own values when
+// given (`trig` = this relation's [cos | sin] row, element k), else rounded
+// once from double.
 template <int M, int MODE>
 __device__ __forceinline__ void ref_make_q(float xa, float xb, float ra, float rb, const Consts& c, float& qa,
-                                           float& qb) {
+                                           float& qb, const float* trig = nullptr, int k = 0, int K = 0) {
   if constexpr (M == ROTATE) {
-    const float th = ra / c.kappa;
-    const float cs = cos_rn(th), sn = sin_rn(th);
-    if constexpr (MODE == HEAD_BATCH) {  // re_r·re_t + im_r·im_t ; re_r·im_t − im_r·re_t
-      qa = cs * xa + sn * xb;
-      qb = cs * xb - sn * xa;
-    } else {                             // re_h·re_r − im_h·im_r ; re_h·im_r + im_h·re_r
-      qa = xa * cs - xb * sn;
-      qb = xa * sn + xb * cs;
+    float cs, sn;
+    if (trig) {
+      cs = trig[k];
+      sn = trig[K + k];
+    } else {
+      const float th = ra / c.kappa;  // model.py:209
+      cs = cos_rn(th);
+      sn = sin_rn(th);
     }
+    Elem<M, MODE>::rotate(xa, xb, cs, sn, qa, qb);  // model.py:215-221
   } else {
     Elem<M, MODE>::make_q(xa, xb, ra, rb, c, qa, qb);  // exact already: no transcendentals
   }

@@ -155,8 +155,10 @@ class RankShardSampler(torch.utils.data.Sampler):
     the first world·⌊n/world⌋.  Every rank's shard has the same length, so the
     ranks' batches have the same size at every step (the factor / owner /
     query-shipping exchanges all-gather per-row buffers of equal shape); the
-    n mod world left-over positions of an epoch's permutation — different
-    ones every epoch — wait for the next.  The ranks' positives are disjoint
+    n mod world positives at the end of an epoch's permutation — different
+    ones every epoch, as each epoch's permutation is drawn independently —
+    are not visited in that epoch.  `seed` must be the same on every rank
+    (run.py broadcasts rank 0's).  The ranks' positives are disjoint
     within an epoch; the epoch advances on every new iteration
     (BidirectionalOneShotIterator restarts the DataLoader endlessly), so no
     set_epoch call is needed.  With world = 1 this is a plain reshuffle per

@@ -108,6 +108,22 @@ def dp_exchange_mode(world: int, override: str | None = None) -> str:
     return mode
 
 
+_OWNER_WARNED = [False]
+
+
+def warn_owner_without_partition() -> None:
+    """The "owner" exchange runs through a partition.EntityRowPartition(model,
+    group, exchange="factors") attached to the model (run.py builds one); a
+    KGEModel trained with a dp_group and no partition falls back to the "grads"
+    exchange — said once, so the exchange in use is never misreported."""
+    if not _OWNER_WARNED[0]:
+        _OWNER_WARNED[0] = True
+        import logging
+        logging.warning('data-parallel exchange "owner" needs EntityRowPartition(model, group, exchange="factors") '
+                        'attached to the model; no partition is attached, so this run uses the "grads" exchange '
+                        '(set KGE_DP_EXCHANGE=grads|factors to choose explicitly)')
+
+
 _FX_BUFS: dict = {}
 
 

@@ -124,15 +124,23 @@ POLL_SPIN_S = 0.05
 def _poll_slot(host: torch.Tensor, dev) -> None:
     """Wait until k_finalize's five floats replaced the NaN sentinel in the
     pinned slot (each is written once, so five non-NaN values are final), or
-    synchronize the device after POLL_SPIN_S (a NaN loss, a slow step)."""
+    synchronize the device after POLL_SPIN_S (a NaN loss, a slow step — a
+    read issued long before its step finishes, e.g. queued behind an
+    evaluation, pays that synchronize).  The first ~64 checks spin (a step's
+    tail is tens of µs); after that the loop yields the GIL between checks."""
     arr = host.numpy()
     if not np.isnan(arr).any():
         return
     t0 = time.perf_counter()
+    spins = 0
     while np.isnan(arr).any():
-        if time.perf_counter() - t0 > POLL_SPIN_S:
+        el = time.perf_counter() - t0
+        if el > POLL_SPIN_S:
             torch.cuda.synchronize(dev)
             return
+        spins += 1
+        if spins > 64:
+            time.sleep(0 if el < 1e-3 else 5e-5)
 
 
 class _LogRing:
@@ -222,6 +230,12 @@ class KGEModel(nn.Module):
         self.keep_grads = True
         # apply a KGEAdam update inside the gradient passes (kge_train_step)
         self.fuse_optimizer = True
+        # RotatE ranking: rotate the queries by the reference's own CPU cos /
+        # sin of the relation phases ("reference", ops.reference_rotation:
+        # ranks bit-exact to the reference's), or by correctly rounded values
+        # evaluated on the device ("device": no host work, last-bit trig
+        # differences can move a near-tied rank)
+        self.rank_trig = "reference"
 
     # ------------------------------------------------------------------ helpers
     def _host_scalars(self):
@@ -237,6 +251,20 @@ class KGEModel(nn.Module):
 
     def _modulus(self):
         return self.modulus if self.model_name == 'pRotatE' else None
+
+    def _rank_rotation(self, dev, relation_trig=None):
+        """The RotatE rotation table a ranking call uses (kge_model_desc.relation_trig):
+        `relation_trig` if given, else per `rank_trig` the reference's CPU cos / sin of
+        the current relation table (evaluated once per call) or None (device trig)."""
+        if self.model_name != 'RotatE':
+            return None
+        if relation_trig is None:
+            if self.rank_trig == "device":
+                return None
+            if self.rank_trig != "reference":
+                raise ValueError("rank_trig %s not supported" % self.rank_trig)
+            relation_trig = ops.reference_rotation(self.relation_embedding, self._host_scalars()[1])
+        return relation_trig.to(dev, torch.float32).contiguous()
 
     def desc(self):
         """The C-ABI model descriptor, rebuilt only when a table moves or is replaced."""
@@ -272,8 +300,8 @@ class KGEModel(nn.Module):
         pos = pos.to(dev)
         neg = None if neg is None else neg.to(dev)
         g, rng = self._host_scalars()
-        return torch.ops.kge.score(self.entity_embedding, self.relation_embedding, pos, neg, mode, self.model_name,
-                                   g, rng, self._modulus())
+        return torch.ops.kge.score(self.entity_embedding, self.relation_embedding, pos, neg, _lib.MODE_IDS[mode],
+                                   _lib.MODEL_IDS[self.model_name], g, rng, self._modulus())
 
     # ------------------------------------------------------- score plug-ins
     def _plugin(self, name, head, relation, tail, mode):
@@ -300,8 +328,8 @@ class KGEModel(nn.Module):
         else:
             raise ValueError('mode %s not supported' % mode)
         g, rng = self._host_scalars()
-        return torch.ops.kge.score(ent.contiguous(), relation.reshape(B, -1).contiguous(), pos, neg, mode, name, g,
-                                   rng, self._modulus())
+        return torch.ops.kge.score(ent.contiguous(), relation.reshape(B, -1).contiguous(), pos, neg,
+                                   _lib.MODE_IDS[mode], _lib.MODEL_IDS[name], g, rng, self._modulus())
 
     def TransE(self, head, relation, tail, mode):
         return self._plugin('TransE', head, relation, tail, mode)
@@ -416,11 +444,14 @@ class KGEModel(nn.Module):
                                       optimizer=optimizer)
         elif dp is not None:
             import torch.distributed as dist
-            from .distributed import dp_exchange_mode, dp_train_grads, dp_train_step_factors
-            if dp_exchange_mode(dist.get_world_size(dp), getattr(args, 'dp_exchange', None)) == "factors":
+            from .distributed import dp_exchange_mode, dp_train_grads, dp_train_step_factors, warn_owner_without_partition
+            exchange = dp_exchange_mode(dist.get_world_size(dp), getattr(args, 'dp_exchange', None))
+            if exchange == "factors":
                 losses = dp_train_step_factors(model, positive_sample, negative_sample, subsampling_weight, mode,
                                                args, optimizer=optimizer)
             else:
+                if exchange == "owner":  # needs the row partition attached (run.py builds it); without one: grads
+                    warn_owner_without_partition()
                 losses = dp_train_grads(model, positive_sample, negative_sample, subsampling_weight, mode, args,
                                         optimizer=optimizer)
         else:
@@ -482,6 +513,7 @@ class KGEModel(nn.Module):
         step = 0
         per_mode = []  # device rank tensors; read back once, after both directions are queued
         with torch.no_grad():
+            trig = model._rank_rotation(dev)
             for mode in ('head-batch', 'tail-batch'):
                 ranks_all = []
                 per_mode.append(ranks_all)
@@ -489,7 +521,7 @@ class KGEModel(nn.Module):
                     q = triples[b0:b0 + block]
                     off, ids = index.filter_csr(q, mode)
                     ranks, _ = ops.rank_filtered(desc, mode, torch.from_numpy(q), torch.from_numpy(off),
-                                                 torch.from_numpy(ids), dev)
+                                                 torch.from_numpy(ids), dev, relation_trig=trig)
                     ranks_all.append(ranks)
                     # progress messages on the reference's batch cadence
                     nb = (len(q) + test_batch_size - 1) // test_batch_size
@@ -512,7 +544,7 @@ class KGEModel(nn.Module):
             'HITS@10': sum(1.0 if r <= 10 else 0.0 for r in ranks_seq) / n,
         }
 
-    def rank_queries_both(self, triples, all_true_triples, path="auto"):
+    def rank_queries_both(self, triples, all_true_triples, path="auto", relation_trig=None):
         """rank_queries for head-batch and tail-batch, both queued before the
         one read-back (the tail direction's host filter CSR overlaps the head
         direction's kernels, as in test_step).  Returns ((ranks, ties) head,
@@ -523,18 +555,20 @@ class KGEModel(nn.Module):
         q = np.asarray(triples, dtype=np.int64).reshape(-1, 3)
         outs = []
         with torch.no_grad():
+            trig = self._rank_rotation(dev, relation_trig)
             for mode in ('head-batch', 'tail-batch'):
                 off, ids = index.filter_csr(q, mode)
                 outs.append(ops.rank_filtered(self.desc(), mode, torch.from_numpy(q), torch.from_numpy(off),
-                                              torch.from_numpy(ids), dev, path=path))
+                                              torch.from_numpy(ids), dev, path=path, relation_trig=trig))
         res = tuple(tuple(t.cpu().numpy() for t in out) for out in outs)
         ops.raise_on_device_error(dev)
         return res
 
-    def rank_queries(self, triples, all_true_triples, mode, path="auto", listed=False):
+    def rank_queries(self, triples, all_true_triples, mode, path="auto", listed=False, relation_trig=None):
         """Per-query filtered ranks and tie counts (numpy int64, int32) — the
         quantity test_step averages; exposed for parity tests and tools.
-        `path` / `listed`: see ops.rank_filtered."""
+        `path` / `listed` / `relation_trig`: see ops.rank_filtered (RotatE:
+        default per `rank_trig`, see _rank_rotation)."""
         dev = ops._require_device(self.entity_embedding)
         index = all_true_triples if isinstance(all_true_triples, FilterIndex) else \
             FilterIndex(all_true_triples, self.nentity, self.nrelation)
@@ -542,7 +576,8 @@ class KGEModel(nn.Module):
         off, ids = index.filter_csr(q, mode)
         with torch.no_grad():
             out = ops.rank_filtered(self.desc(), mode, torch.from_numpy(q), torch.from_numpy(off),
-                                    torch.from_numpy(ids), dev, path=path, listed=listed)
+                                    torch.from_numpy(ids), dev, path=path, listed=listed,
+                                    relation_trig=self._rank_rotation(dev, relation_trig))
         res = tuple(t.cpu().numpy() for t in out)
         ops.raise_on_device_error(dev)
         return res

@@ -54,7 +54,9 @@ class _DeviceState:
     def __init__(self, dev: torch.device):
         self.dev = dev
         self.ws = {}
-        self.err = torch.zeros(1, dtype=torch.int32, device=dev)
+        # the flag the torch.ops.kge.* kernels OR into too (one per device)
+        from . import torch_ops  # noqa: F401  (loads libkge_torch.so)
+        self.err = torch.ops.kge.error_flag(dev)
 
     def workspace(self, nbytes: int) -> torch.Tensor:
         s = torch.cuda.current_stream(self.dev)
@@ -385,17 +387,45 @@ def adam_step(param: torch.Tensor, grad: torch.Tensor, exp_avg: torch.Tensor, ex
 RANK_PATHS = {"auto": 0, "mfma": 1, "tile": 2, "scan": 3}
 
 
+def reference_rotation(relation: torch.Tensor, embedding_range: float) -> torch.Tensor:
+    """RotatE's relation rotations as the reference evaluates them: [R, 2, d]
+    (cos θ | sin θ) of θ = relation / (embedding_range / π), by the
+    reference's own ATen CPU ops (model.py:209-212) — the table
+    kge_model_desc.relation_trig carries into the filtered ranking.
+
+    Only this [R, d] table is evaluated on the host, once per ranking call:
+    the reference's ranks are defined by its CPU vector library's cos / sin,
+    which no device instruction sequence reproduces bit for bit (they differ
+    from correctly rounded values on ~5 % of arguments).  Elementwise, so the
+    whole table gives the same bits as the reference's gathered [B, 1, d]
+    rows (tests/test_rank_parity_gpu.py checks the host's bits against the
+    reference's, committed in tests/golden/rotate_trig.npz)."""
+    rel = relation.detach().to("cpu", torch.float32)
+    phase = rel / (embedding_range / PI)
+    return torch.stack([torch.cos(phase), torch.sin(phase)], 1).contiguous()
+
+
 def rank_filtered(desc: _lib.ModelDesc, mode: str, queries: torch.Tensor, filt_off: torch.Tensor,
-                  filt_ids: torch.Tensor, dev, path: str = "auto", listed: bool = False):
+                  filt_ids: torch.Tensor, dev, path: str = "auto", listed: bool = False,
+                  relation_trig: Optional[torch.Tensor] = None):
     """Filtered ranks (int64) and tie counts (int32) for a block of queries
     (model.py:383-418), in the reference's fp32 score order
     (kge_rank_filtered_ex).  `path` picks the fast counting pass ("auto",
     "mfma", "tile", "scan"); `listed` also returns the per-query number of
-    near-ties that were re-scored."""
+    near-ties that were re-scored; `relation_trig` (RotatE, [R, 2, d] on the
+    device, see reference_rotation) is the rotation table the ranks are
+    computed with (None: correctly rounded cos / sin)."""
     if mode not in ("head-batch", "tail-batch"):
         raise ValueError("mode %s not supported" % mode)
     if path not in RANK_PATHS:
         raise ValueError("rank path %s not supported" % path)
+    if relation_trig is not None:
+        shape = (desc.nrelation, 2, desc.relation_dim)
+        if (tuple(relation_trig.shape) != shape or relation_trig.dtype != torch.float32
+                or not relation_trig.is_contiguous() or relation_trig.device != dev):
+            raise ValueError(f"relation_trig: expected a contiguous float32 {shape} tensor on {dev}")
+        desc = _lib.ModelDesc.from_buffer_copy(desc)
+        desc.relation_trig = relation_trig.data_ptr()
     q = _idx(queries, dev)
     off = _idx(filt_off, dev)
     ids = _idx(filt_ids, dev) if filt_ids.numel() else torch.zeros(1, dtype=torch.int64, device=dev)

@@ -110,6 +110,10 @@ class EntityRowPartition:
         self.lo = self.rank * self.rows
         self.hi = min(E, self.lo + self.rows)
         self.nown = max(0, self.hi - self.lo)  # the last shards may be short (or empty)
+        # the owned entity rows as a valid range of [0, E): a trailing rank of a
+        # small table can start past E (E = 5, world 4: lo = 6), its range is then empty
+        self.e0 = min(self.lo, E)
+        self.e1 = self.e0 + self.nown
         dev = ent.device
         self._pending = []  # (all-gather work, staging buffer, shard rows c0, c1) of the owner step's chunks
         self._stage = {}
@@ -235,7 +239,7 @@ class EntityRowPartition:
         from . import ops
         dev = model.entity_embedding.device
         fx = _dist._exchange_row_factors(model, positive_sample, negative_sample, subsampling_weight, mode, args,
-                                         csr_range=(min(self.lo, self.nentity), min(self.lo, self.nentity) + self.nown))
+                                         csr_range=(self.e0, self.e1))
         adam = None
         if optimizer is not None and model.fuse_optimizer and hasattr(optimizer, 'prepare_fused_rows'):
             adam = optimizer.prepare_fused_rows(self.shard, model.entity_embedding, self.lo,
@@ -247,22 +251,22 @@ class EntityRowPartition:
                   adam=adam, csr_ready=_dist.FX_CSR_AHEAD, workspace=fx.workspace, reg_relations=self.rank == 0)
         desc = model.desc()
         chunks = self._owner_chunks() if adam is not None else []
+        own = (self.e0, self.e1)
         if len(chunks) <= 1:
-            ops.train_step_from_rows(desc, mode, fx.pos, fx.neg, fx.w, fx.wsum, dev, entity_range=(self.lo, self.hi),
-                                     **kw)
+            ops.train_step_from_rows(desc, mode, fx.pos, fx.neg, fx.w, fx.wsum, dev, entity_range=own, **kw)
         else:
             # the entity pass + fused Adam of the owned rows in chunks; chunk
             # c's all-gather (every rank's rows c0..c1 of its shard) is on the
             # wire while chunk c+1 is computed; gather() places them
-            ops.train_step_from_rows(desc, mode, fx.pos, fx.neg, fx.w, fx.wsum, dev, entity_range=(self.lo, self.hi),
+            ops.train_step_from_rows(desc, mode, fx.pos, fx.neg, fx.w, fx.wsum, dev, entity_range=own,
                                      phases=_lib_phase("ROWS"), **kw)
             for c0, c1 in chunks:
-                e0, e1 = self.lo + c0, min(self.hi, self.lo + c1)
+                e0, e1 = min(self.e1, self.e0 + c0), min(self.e1, self.e0 + c1)
                 if e1 > e0:
                     ops.train_step_from_rows(desc, mode, fx.pos, fx.neg, fx.w, fx.wsum, dev, entity_range=(e0, e1),
                                              phases=_lib_phase("ENTITY"), **kw)
                 self.put_chunk(c0, c1)
-            ops.train_step_from_rows(desc, mode, fx.pos, fx.neg, fx.w, fx.wsum, dev, entity_range=(self.lo, self.hi),
+            ops.train_step_from_rows(desc, mode, fx.pos, fx.neg, fx.w, fx.wsum, dev, entity_range=own,
                                      phases=_lib_phase("FINALIZE"), **kw)
         # the owner's rows of the gradient; the replica itself is not optimised
         self.shard.grad = self.grad_full[self.lo:self.lo + self.rows] if adam is None or model.keep_grads else None
@@ -435,6 +439,6 @@ class EntityRowPartition:
             for k in ('exp_avg', 'exp_avg_sq'):
                 full = st[k]
                 part = torch.zeros(self.rows, self.dim, dtype=full.dtype)
-                part[:self.hi - self.lo] = full[self.lo:self.hi]
+                part[:self.nown] = full[self.e0:self.e1]
                 st[k] = part
         optimizer.load_state_dict(sd)

@@ -132,20 +132,34 @@ def read_dict(file_path):
     return out
 
 
-def make_train_iterator(args, train_triples, nentity, nrelation, rank=0, world=1):
+def shared_seed(group=None) -> int:
+    """A sampler seed that is the same on every rank: rank 0's torch seed,
+    broadcast (a per-rank seed would make the ranks' shards of an epoch
+    overlap or skip positives, undetected)."""
+    import torch.distributed as dist
+    seed = [int(torch.initial_seed()) % (1 << 31)]
+    if dist.is_available() and dist.is_initialized():
+        dist.broadcast_object_list(seed, src=dist.get_global_rank(group, 0) if group is not None else 0,
+                                   group=group)
+    return int(seed[0])
+
+
+def make_train_iterator(args, train_triples, nentity, nrelation, rank=0, world=1, seed=None):
     """run.py:246-259's two DataLoaders and BidirectionalOneShotIterator.  One
     process: exactly the reference's (shuffle=True on torch's global
     generator).  Under data parallelism each rank gets a disjoint shard of
-    every epoch's permutation (RankShardSampler, same seed on all ranks) and
-    its own generator, so its workers' numpy streams — the negatives — differ
-    from the other ranks' too."""
+    every epoch's permutation (RankShardSampler, `seed` — shared_seed() by
+    default — the same on all ranks) and its own generator, so its workers'
+    numpy streams — the negatives — differ from the other ranks' too."""
+    if world > 1 and seed is None:
+        seed = shared_seed(getattr(args, 'dp_group', None))
+
     def loader(mode):
         ds = TrainDataset(train_triples, nentity, nrelation, args.negative_sample_size, mode)
         kw = dict(batch_size=args.batch_size, num_workers=max(1, args.cpu_num // 2),
                   collate_fn=TrainDataset.collate_fn)
         if world <= 1:
             return DataLoader(ds, shuffle=True, **kw)
-        seed = int(torch.initial_seed()) % (1 << 31)
         return DataLoader(ds, sampler=RankShardSampler(len(ds), rank, world, seed + (mode == 'tail-batch')),
                           generator=torch.Generator().manual_seed(seed + 7919 * (rank + 1)), **kw)
 
@@ -262,8 +276,8 @@ def main(args):
         exchange = os.environ.get('KGE_PART_EXCHANGE', 'factors') if getattr(args, 'row_partition', False) \
             else 'factors'
         part = EntityRowPartition(kge_model, args.dp_group, exchange=exchange)
-        logging.info('Entity rows partitioned (%s exchange): rank %d owns [%d, %d)' % (exchange, rank, part.lo,
-                                                                                        part.hi))
+        logging.info('Entity rows partitioned (%s exchange): rank %d owns [%d, %d)' % (exchange, rank, part.e0,
+                                                                                        part.e1))
 
     def trainable():
         return part.parameters() if part is not None else filter(lambda p: p.requires_grad, kge_model.parameters())
@@ -278,13 +292,14 @@ def main(args):
         if part is not None:
             part.materialize() if on else part.release()
 
+    world = 1 if args.dp_group is None else torch.distributed.get_world_size(args.dp_group)
     if args.do_train and getattr(args, 'device_sampler', False):
         from .sampler import DeviceTrainIterator
         train_iterator = DeviceTrainIterator(train_triples, nentity, nrelation, args.negative_sample_size,
                                              args.batch_size, kge_model.entity_embedding.device,
-                                             seed=torch.initial_seed() + rank)
+                                             seed=torch.initial_seed() + rank, rank=rank, world=world,
+                                             perm_seed=shared_seed(args.dp_group) if world > 1 else None)
     elif args.do_train:
-        world = 1 if args.dp_group is None else torch.distributed.get_world_size(args.dp_group)
         train_iterator = make_train_iterator(args, train_triples, nentity, nrelation, rank, world)
     if args.do_train:
         current_learning_rate = args.learning_rate

@@ -93,10 +93,17 @@ class DeviceTrainIterator:
     """``next()`` → (positive_sample [B,3] int64, negative_sample [B,n] int64,
     subsampling_weight [B] fp32, mode), all on `device`, tail-batch first and
     then alternating — BidirectionalOneShotIterator's protocol
-    (dataloader.py:165-186) over two shuffled TrainDataset loaders."""
+    (dataloader.py:165-186) over two shuffled TrainDataset loaders.
+
+    Data parallel (world > 1): every rank draws the same per-epoch permutation
+    (from `perm_seed`, which must be equal on all ranks) and takes positions
+    rank, rank + world, ... of its first world·⌊T/world⌋ — disjoint shards of
+    equal length, as RankShardSampler gives the host loaders; the negatives'
+    streams are keyed by the rank's own `seed`."""
 
     def __init__(self, train_triples, nentity: int, nrelation: int, negative_sample_size: int, batch_size: int,
-                 device, seed: int = 0, max_draws: int | None = None):
+                 device, seed: int = 0, max_draws: int | None = None, rank: int = 0, world: int = 1,
+                 perm_seed: int | None = None):
         dev = torch.device(device)
         ops._require_device(torch.empty(0, device=dev))
         self.lists = TrueLists(train_triples, nentity, nrelation)
@@ -114,8 +121,11 @@ class DeviceTrainIterator:
                                      torch.from_numpy(ids).to(dev) if len(ids) else torch.zeros(1, dtype=torch.int64,
                                                                                                 device=dev))
         self.seed = int(seed)
+        if world < 1 or not 0 <= rank < world:
+            raise ValueError(f"rank {rank} outside world {world}")
+        self.rank, self.world = int(rank), int(world)
         self.gen = torch.Generator(device=dev)
-        self.gen.manual_seed(self.seed)
+        self.gen.manual_seed(self.seed if perm_seed is None else int(perm_seed))
         self._perm = {'head-batch': None, 'tail-batch': None}
         self._cursor = {'head-batch': 0, 'tail-batch': 0}
         self.step = 0
@@ -125,9 +135,10 @@ class DeviceTrainIterator:
         return self
 
     def _indices(self, mode: str) -> torch.Tensor:
-        T = self.triples.shape[0]
+        T = self.triples.shape[0] // self.world  # this rank's shard of an epoch
         if self._perm[mode] is None or self._cursor[mode] >= T:  # a new epoch of this loader
-            self._perm[mode] = torch.randperm(T, device=self.dev, generator=self.gen)
+            perm = torch.randperm(self.triples.shape[0], device=self.dev, generator=self.gen)
+            self._perm[mode] = perm[self.rank:self.world * T:self.world]
             self._cursor[mode] = 0
         c = self._cursor[mode]
         self._cursor[mode] = c + self.batch_size

@@ -43,6 +43,8 @@ def _desc(model=3, le=16, lr=8, ne=10, nr=3):
     (2, 16, 8, 3),     # ComplEx needs -de and -dr, model.py:69-70
     (0, 16, 8, 3),     # TransE rows must broadcast
     (1, 8192, 8192, 6),  # beyond the compiled row range
+    (1, 2049, 2049, 6),  # (half-)rows up to 2048 floats, any alignment (2049: one past)
+    (3, 4098, 2049, 6),
 ])
 def test_model_validation(model, le, lr, status):
     lib = _lib.load()

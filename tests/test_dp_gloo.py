@@ -200,3 +200,32 @@ def test_factor_exchange_gathers_global_batch(uni, world):
             assert s["slice"][1] == pytest.approx(float(w.sum())) and s["global_scalars"][2] == s["slice"][1]
     for rank in range(1, world):
         assert torch.equal(out[0]["losses"], out[rank]["losses"])
+
+
+def _shard_worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from knowledgegraphembedding_amd.dataloader import RankShardSampler
+    from knowledgegraphembedding_amd.run import shared_seed
+    torch.manual_seed(1000 + 17 * rank)  # every rank's own torch seed differs
+    seed = shared_seed(dist.group.WORLD)
+    sampler = RankShardSampler(103, rank, world, seed)
+    out[rank] = (seed, list(sampler), list(sampler))  # two epochs
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_rank_shards_disjoint_with_per_rank_torch_seeds(world):
+    """the sampler seed is rank 0's, broadcast, so even with
+    different torch seeds per rank one epoch's shards are disjoint, equally
+    long and cover world·⌊n/world⌋ positives; the next epoch reshuffles."""
+    out = mp.Manager().dict()
+    mp.spawn(_shard_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    seeds = {out[r][0] for r in range(world)}
+    assert len(seeds) == 1
+    for ep in (1, 2):
+        shards = [out[r][ep] for r in range(world)]
+        assert all(len(s) == 103 // world for s in shards)
+        union = set().union(*map(set, shards))
+        assert len(union) == world * (103 // world)
+    assert out[0][1] != out[0][2]

@@ -34,16 +34,16 @@ def _free_port():
     return p
 
 
-def _model(name):
+def _model(name, e=E):
     torch.manual_seed(0)
     de, dr = DIMS[name]
-    return KGEModel(name, E, R, D, GAMMA, de, dr).to("cuda:0")
+    return KGEModel(name, e, R, D, GAMMA, de, dr).to("cuda:0")
 
 
-def _batches(dev):
+def _batches(dev, e=E):
     out = []
     for k, mode in enumerate(("tail-batch", "head-batch", "tail-batch")):
-        pos, neg, w = synth.kge_batch(80 + k, B, N, E, R)
+        pos, neg, w = synth.kge_batch(80 + k, B, N, e, R)
         out.append((torch.from_numpy(pos).to(dev), torch.from_numpy(neg).to(dev), torch.from_numpy(w).to(dev), mode))
     return out
 
@@ -53,43 +53,45 @@ def _args(group, reg, uni):
                      regularization=reg, dp_group=group)
 
 
-def _worker(rank, world, port, name, reg, uni, chunks, out):
+def _worker(rank, world, port, name, reg, uni, chunks, e, out):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     torch.cuda.set_device(0)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from knowledgegraphembedding_amd import partition
     from knowledgegraphembedding_amd.partition import EntityRowPartition
     partition.OWNER_CHUNKS = chunks
-    model = _model(name)
+    model = _model(name, e)
     part = EntityRowPartition(model, dist.group.WORLD, exchange="factors")
     opt = KGEAdam(part.parameters(), lr=LR)
     sl = slice(rank * B // world, (rank + 1) * B // world)
-    it = iter([(p[sl], n[sl], w[sl], m) for p, n, w, m in _batches("cuda:0")])
+    it = iter([(p[sl], n[sl], w[sl], m) for p, n, w, m in _batches("cuda:0", e)])
     logs = [dict(KGEModel.train_step(model, opt, it, _args(dist.group.WORLD, reg, uni))) for _ in range(3)]
     torch.cuda.synchronize()
     st = opt.state[part.shard]
     out[rank] = {"logs": logs, "ent": model.entity_embedding.detach().cpu().numpy(),
-                 "rel": model.relation_embedding.detach().cpu().numpy(), "lo": part.lo, "hi": part.hi,
-                 "m": st["exp_avg"][:part.hi - part.lo].cpu().numpy(),
-                 "v": st["exp_avg_sq"][:part.hi - part.lo].cpu().numpy(),
+                 "rel": model.relation_embedding.detach().cpu().numpy(), "lo": part.e0, "hi": part.e1,
+                 "m": st["exp_avg"][:part.nown].cpu().numpy(),
+                 "v": st["exp_avg_sq"][:part.nown].cpu().numpy(),
                  "mod": model.modulus.detach().cpu().numpy() if name == "pRotatE" else None}
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("name,reg,uni,world,chunks", [("RotatE", 0.0, False, 2, 4), ("RotatE", 0.0, False, 4, 4),
-                                                       ("RotatE", 0.0, False, 2, 1), ("ComplEx", 1e-4, False, 4, 4),
-                                                       ("pRotatE", 0.0, True, 2, 4), ("TransE", 0.0, False, 4, 1),
-                                                       ("DistMult", 1e-4, True, 2, 3)])
-def test_owner_exchange_bitwise(name, reg, uni, world, chunks):
+@pytest.mark.parametrize("name,reg,uni,world,chunks,e", [("RotatE", 0.0, False, 2, 4, E), ("RotatE", 0.0, False, 4, 4, E),
+                                                         ("RotatE", 0.0, False, 2, 1, E), ("ComplEx", 1e-4, False, 4, 4, E),
+                                                         ("pRotatE", 0.0, True, 2, 4, E), ("TransE", 0.0, False, 4, 1, E),
+                                                         ("DistMult", 1e-4, True, 2, 3, E), ("RotatE", 1e-4, False, 4, 4, 5)])
+def test_owner_exchange_bitwise(name, reg, uni, world, chunks, e):
     """chunks > 1: the owned rows' pass in chunks (kge_train_step_from_rows_phased),
     each chunk's all-gather issued before the next chunk runs (151 owned rows
     at world 2 give 4 chunks, 76 at world 4 give 2); 1: one call and one
-    all-gather.  Both bit-identical to one process."""
+    all-gather.  Both bit-identical to one process.  e = 5 at world 4: shards
+    of 2 rows, rank 2 owns one row and rank 3 starts past the table (lo = 6),
+    so its range is empty (the owner step clamps it)."""
     out = mp.Manager().dict()
-    mp.spawn(_worker, args=(world, _free_port(), name, reg, uni, chunks, out), nprocs=world, join=True)
-    model = _model(name)
+    mp.spawn(_worker, args=(world, _free_port(), name, reg, uni, chunks, e, out), nprocs=world, join=True)
+    model = _model(name, e)
     opt = KGEAdam([p for p in model.parameters() if p.requires_grad], lr=LR)
-    it = iter(_batches("cuda:0"))
+    it = iter(_batches("cuda:0", e))
     ref = [dict(KGEModel.train_step(model, opt, it, _args(None, reg, uni))) for _ in range(3)]
     ent = model.entity_embedding.detach().cpu().numpy()
     rel = model.relation_embedding.detach().cpu().numpy()

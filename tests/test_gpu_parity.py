@@ -123,6 +123,45 @@ def test_train_step_vs_golden(g_train, golden_info):
         assert np.abs(p2 - r2).max() <= 2e-4 * 0.01 * 2 + 1e-6, f"{case} params after 2 steps"
 
 
+@pytest.mark.parametrize("name,d", [("DistMult", 2000), ("TransE", 1001), ("RotatE", 1001), ("ComplEx", 2047),
+                                    ("pRotatE", 1999), ("DistMult", 2048), ("RotatE", 2000)])
+def test_wide_and_odd_dims_vs_oracle(name, d):
+    """Any hidden_dim up to 2048 floats per (half-)row: best_config.sh:44-50's
+    DistMult d = 2000, odd / unaligned d (the single-float slot kernels with 16
+    or 32 slots per lane) — scores, the fused train step's losses and
+    gradients in both modes, and filtered ranks against the oracle."""
+    E, R, B, n, gamma = 150, 5, 6, 12, 9.0
+    m, ent, rel, mod, rng = build_model(name, E, R, d, gamma, 17)
+    pos, neg, w = synth.kge_batch(18, B, n, E, R)
+    P, N = torch.from_numpy(pos), torch.from_numpy(neg)
+    g = torch.Tensor([gamma]).item()
+    modt = None if mod is None else torch.from_numpy(mod)
+    E_, R_ = torch.from_numpy(ent), torch.from_numpy(rel)
+    with torch.no_grad():
+        for mode in ("single", "head-batch", "tail-batch"):
+            ref = O.forward(name, E_, R_, modt, P if mode == "single" else (P, N), mode, g, rng).numpy()
+            s = (m(P.to(DEV)) if mode == "single" else m((P.to(DEV), N.to(DEV)), mode)).cpu().numpy()
+            assert np.all(np.abs(s - ref) <= score_tol(ref)), f"{name} d={d} {mode}"
+    args = Namespace(negative_adversarial_sampling=True, adversarial_temperature=1.0, uni_weight=False,
+                     regularization=1e-4 if name in ("DistMult", "ComplEx") else 0.0)
+    for mode in ("head-batch", "tail-batch"):
+        losses = m.compute_train_grads(P.to(DEV), N.to(DEV), torch.from_numpy(w).to(DEV), mode, args).cpu().numpy()
+        ops.raise_on_device_error(DEV)
+        log, ge, gr, gm = O.train_grads(name, E_, R_, modt, P, N, torch.from_numpy(w), mode, adversarial=True,
+                                        temperature=1.0, uni_weight=False, regularization=args.regularization,
+                                        gamma=g, erange=rng)
+        ref = np.array([log["positive_sample_loss"], log["negative_sample_loss"], log["loss"]])
+        assert np.all(np.abs(losses[:3] - ref) <= score_tol(ref)), f"{name} d={d} {mode} losses"
+        assert_close_grad(m.entity_embedding.grad.cpu().numpy(), ge.numpy(), f"{name} d={d} {mode} ent")
+        assert_close_grad(m.relation_embedding.grad.cpu().numpy(), gr.numpy(), f"{name} d={d} {mode} rel")
+    if name != "pRotatE":  # (pRotatE's sin is correctly rounded here: ranks are checked in test_rank_parity_gpu)
+        triples = pos.tolist()
+        for mode in ("head-batch", "tail-batch"):
+            ranks, _ = m.rank_queries(triples, triples, mode)
+            oref = O.filtered_ranks(name, E_, R_, modt, triples, triples, mode, g, rng)
+            assert np.array_equal(ranks, oref["rank_count"]), (name, d, mode, ranks, oref["rank_count"])
+
+
 @pytest.mark.parametrize("name", NAMES)
 @pytest.mark.parametrize("mode", ["head-batch", "tail-batch"])
 def test_train_grads_vs_oracle_realistic(name, mode):

@@ -5,31 +5,33 @@ real wn18rr split with DistMult / ComplEx / pRotatE at d = 500 and E = 40943,
 the FB15k entity set with TransE / RotatE at d = 1000).
 
 What is asserted, per query (rank = 1 + #{unfiltered e ≠ true: s_e > s_true}):
-  * TransE, DistMult, ComplEx: the kernel's near-ties are re-scored in the
-    reference's fp32 operation order (kge_rank_ref.h), so ranks AND tie counts
-    equal the reference's on every query; where the reference has exact ties
-    (its argsort is not stable) its position lies in [rank, rank + ties].
-  * RotatE, pRotatE: identical except the reference's CPU cos/sin (vs
-    correctly rounded here).  A query is decidable when no competitor of the
-    reference lies within the rigorous bound δ of what last-bit trig
-    differences can move a gap (below); decidable queries must match exactly,
-    the others within the number of competitors inside δ.  The reference's
-    CPU build evaluates cos/sin with MKL's vector library (tests: not the
-    bundled SLEEF — it differs from torch.cos on 2-3 % of arguments, as do
-    correctly rounded values on ~5 %), which cannot be reproduced here; at the
-    FB15k scale this moves ~3 % of RotatE ranks.  Queries without a reference
-    tie that differ: none for the exact models, ≤ 5 % for RotatE / pRotatE.
+  * TransE, DistMult, ComplEx, RotatE: the kernel's near-ties are re-scored in
+    the reference's fp32 operation order (kge_rank_ref.h), so ranks AND tie
+    counts equal the reference's on every query; where the reference has exact
+    ties (its argsort is not stable) its position lies in [rank, rank + ties].
+    RotatE's rotation comes from the reference's own cos / sin bits of the
+    relation phases (tests/golden/rotate_trig.npz, made by the reference's
+    ATen CPU ops in make_golden.py `gen_rotate_trig`), fed to the kernels as
+    kge_model_desc.relation_trig — the table KGEModel builds itself with
+    ops.reference_rotation on the host it runs on.
+  * pRotatE: its sin acts on per-candidate phase sums (model.py:241-245), so
+    no table can carry the reference's values; correctly rounded sin here.  A
+    query is decidable when no competitor of the reference lies within the
+    rigorous bound δ of what last-bit sin differences can move a gap (below);
+    decidable queries must match exactly, the others within the number of
+    competitors inside δ, and at most 5 % of the untied queries may differ.
   * Every fast path (MFMA tile, register tile, wave scan) returns the same
     ranks and ties bit for bit: their windows differ, the refinement does not.
+  * test_host_trig_matches_reference: this host's torch.cos / torch.sin (what
+    KGEModel.test_step uses) against the reference's committed bits; if they
+    differ, the reference's RotatE ranks depend on the CPU's vector library,
+    and the test reports by how much (ranks from this host's table against
+    the reference's).
 
-δ for RotatE (u = 2^-24, K complex dims, S = γ − s_true, Q1 = Σ|x| over the
-anchor row): each trig value may move by 1 ulp, i.e. each q component by
-≤ 4u·(|x_re| + |x_im|); an element (Lipschitz 1 in q) by that plus 4u of
-itself; every partial sum of the reference's reduction (≤ K/32 + 24 per lane
+δ for pRotatE (u = 2^-24, K dims, S = (γ − s_true)/mod): |sin| moves by ≤ u per
+element; every partial sum of the reference's reduction (≤ K/32 + 24 per lane
 column and fold) may round the other way by ≤ 2u of its value; both the
-candidate and the true score move:  δ = 2·(8u·Q1 + (4 + 2·(K/32 + 24))·u·S).
-pRotatE: |sin| moves by ≤ u per element:  δ = 2·mod·(K·u + (4 + 2·(K/32 + 24))·u·S),
-S = (γ − s_true)/mod.
+candidate and the true score move:  δ = 2·mod·(K·u + (4 + 2·(K/32 + 24))·u·S).
 """
 import numpy as np
 import pytest
@@ -41,7 +43,7 @@ from knowledgegraphembedding_amd import KGEModel
 pytestmark = pytest.mark.gpu
 DEV = torch.device("cuda", 0)
 U = 2.0 ** -24
-EXACT = ("TransE", "DistMult", "ComplEx")
+EXACT = ("TransE", "DistMult", "ComplEx", "RotatE")
 PATHS = {"DistMult": ("auto", "tile", "scan"), "ComplEx": ("auto", "tile", "scan"),
          "TransE": ("auto", "scan"), "RotatE": ("auto", "scan"), "pRotatE": ("auto", "scan")}
 
@@ -53,20 +55,30 @@ def build(name, E, R, d, gamma, seed):
     with torch.no_grad():
         m.entity_embedding.copy_(torch.from_numpy(ent))
         m.relation_embedding.copy_(torch.from_numpy(rel))
-    return m.to(DEV), ent, mod
+    return m.to(DEV), ent, rel, mod, rng
 
 
-def trig_bound(name, ent, mod, queries, mode, d, gamma, s_true):
-    """δ above (0 for the models without transcendentals)."""
+def reference_trig(tag, rel, rng):
+    """[R, 2, d] reference (cos | sin) of the relation phases: the committed
+    XOR (rotate_trig.npz) applied to correctly rounded values for the queried
+    relations (the others are never read by the fixture's queries); plus the
+    phases, computed as model.py:209 does (an IEEE division, host-independent)."""
+    g = load_npz("rotate_trig.npz")
+    phase = (torch.from_numpy(rel) / (rng / 3.14159265358979323846)).numpy()
+    ph64 = phase.astype(np.float64)
+    cs, sn = np.cos(ph64).astype(np.float32), np.sin(ph64).astype(np.float32)
+    ids = g[f"{tag}/rel_ids"]
+    cs.view(np.uint32)[ids] ^= g[f"{tag}/cos_xor"]
+    sn.view(np.uint32)[ids] ^= g[f"{tag}/sin_xor"]
+    return torch.from_numpy(np.stack([cs, sn], 1)), phase, ids
+
+
+def trig_bound(name, mod, queries, d, gamma, s_true):
+    """δ above (0 for the models whose operations are all reproduced)."""
     if name in EXACT:
         return np.zeros(len(queries))
     K = d
     fold = 4 + 2 * (K / 32 + 24)
-    if name == "RotatE":
-        anchor = queries[:, 2] if mode == "head-batch" else queries[:, 0]
-        q1 = np.abs(ent[anchor].astype(np.float64)).sum(1)
-        S = np.abs(gamma - s_true.astype(np.float64))
-        return 2 * (8 * U * q1 + fold * U * S)
     m = float(mod[0, 0])
     S = np.abs(gamma - s_true.astype(np.float64)) / m
     return 2 * m * (K * U + fold * U * S)
@@ -88,7 +100,7 @@ def check(tag, name, mode, ranks, ties, ref, bound):
     differ = ranks != r_rank
     # a query the reference ties at the true score is placed by its non-stable
     # argsort somewhere in [rank, rank + ties] (checked above); the others may
-    # differ only through the trig bound, and on at most 1 % of the queries
+    # differ only through pRotatE's sin bound, and on at most 5 % of the queries
     untied_differ = int((differ & (r_ties == 0)).sum())
     cap = 0 if name in EXACT else 0.05 * len(ranks)
     assert untied_differ <= cap, f"{tag} {name} {mode}: {untied_differ} of {len(ranks)} ranks differ"
@@ -96,15 +108,16 @@ def check(tag, name, mode, ranks, ties, ref, bound):
 
 
 def run_case(tag, name, E, R, d, gamma, seed, queries, filters, refs, report):
-    m, ent, mod = build(name, E, R, d, gamma, seed)
+    m, ent, rel, mod, rng = build(name, E, R, d, gamma, seed)
+    trig = reference_trig(tag, rel, rng)[0] if name == "RotatE" else None
     for mode in ("head-batch", "tail-batch"):
         ref = refs(mode)
         nq = len(ref["rank"])
         qs = queries[:nq]
-        bound = trig_bound(name, ent, mod, qs, mode, d, gamma, ref["s_true"])
+        bound = trig_bound(name, mod, qs, d, gamma, ref["s_true"])
         base = None
         for path in PATHS[name]:
-            ranks, ties, listed = m.rank_queries(qs, filters, mode, path=path, listed=True)
+            ranks, ties, listed = m.rank_queries(qs, filters, mode, path=path, listed=True, relation_trig=trig)
             if base is None:
                 base = (ranks, ties)
             else:
@@ -166,3 +179,36 @@ def test_ranks_vs_reference_full_size(g_full, golden_info, case):
     run_case(tag, name, kg["E"], kg["R"], mdl["d"], gamma, kg["seed"], g_full[f"{tag}/queries"],
              g_full[f"{tag}/filters"], refs, report)
     _print(report)
+
+
+def test_host_trig_matches_reference(g_full, golden_info, capsys):
+    """This host's torch.cos / torch.sin of the FB15k fixture's relation phases
+    (what KGEModel.test_step rotates RotatE's queries by, ops.reference_rotation)
+    against the reference's bits.  Equal: test_step's RotatE ranks on this host
+    are the reference's.  Different: the reference's own ranks depend on the
+    CPU's vector library; the test then reports how many fixture ranks this
+    host's table moves (asserting only that the committed-bit ranks above are
+    exact, which test_ranks_vs_reference_full_size does)."""
+    from knowledgegraphembedding_amd import ops
+    kg = next(k for k in golden_info["ranks_full"] if k["tag"] == "fb15k")
+    d, gamma = 1000, torch.Tensor([kg["gamma"]]).item()
+    m, ent, rel, mod, rng = build("RotatE", kg["E"], kg["R"], d, gamma, kg["seed"])
+    ref_tab, phase, ids = reference_trig("fb15k", rel, rng)
+    host_tab = ops.reference_rotation(torch.from_numpy(rel), m._host_scalars()[1])
+    same = (host_tab.numpy().view(np.uint32)[ids] == ref_tab.numpy().view(np.uint32)[ids])
+    frac = 1.0 - float(same.mean())
+    with capsys.disabled():
+        print(f"\nhost torch.cos/sin vs the reference's bits on {same.size} fixture values: {frac:.4%} differ "
+              f"(MKL {torch.backends.mkl.is_available()}, cpu capability "
+              f"{torch.backends.cpu.get_cpu_capability()})")
+    if frac == 0.0:
+        return
+    # the bits differ: measure what this host's table does to the reference's ranks (reported, not asserted)
+    nq = len(g_full["fb15k/RotatE/head-batch/rank"])
+    qs, filters = g_full["fb15k/queries"][:nq], g_full["fb15k/filters"]
+    for mode in ("head-batch", "tail-batch"):
+        ranks, _ = m.rank_queries(qs, filters, mode, relation_trig=host_tab)
+        r_rank = g_full[f"fb15k/RotatE/{mode}/rank"]
+        with capsys.disabled():
+            print(f"  {mode}: ranks from this host's cos/sin differ from the reference's on "
+                  f"{int((ranks != r_rank).sum())} of {nq} queries")

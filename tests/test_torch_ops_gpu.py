@@ -11,6 +11,7 @@ import torch
 from conftest import synth_tables
 from knowledgegraphembedding_amd import KGEModel, synth
 from knowledgegraphembedding_amd.filters import FilterIndex
+from knowledgegraphembedding_amd.torch_ops import MODE_IDS, MODEL_IDS
 
 pytestmark = pytest.mark.gpu
 DEV = torch.device("cuda", 0)
@@ -34,16 +35,25 @@ def test_opcheck(name):
     ent = m.entity_embedding.detach().clone().requires_grad_(True)
     rel = m.relation_embedding.detach().clone().requires_grad_(True)
     mod = m.modulus.detach().clone().requires_grad_(True) if name == "pRotatE" else None
+    mid = MODEL_IDS[name]
     for mode, nn_ in (("tail-batch", neg), ("head-batch", neg), ("single", None)):
-        torch.library.opcheck(torch.ops.kge.score.default, (ent, rel, pos, nn_, mode, name, g, rng, mod))
+        torch.library.opcheck(torch.ops.kge.score.default, (ent, rel, pos, nn_, MODE_IDS[mode], mid, g, rng, mod))
     torch.library.opcheck(torch.ops.kge.train_step_grads.default,
                           (ent.detach(), rel.detach(), None if mod is None else mod.detach(), pos, neg, w,
-                           "tail-batch", name, g, rng, True, 1.0, False, 0.0))
+                           MODE_IDS["tail-batch"], mid, g, rng, True, 1.0, False, 0.0))
     idx = FilterIndex(pos.cpu().numpy().tolist(), 500, 9)
     off, ids = idx.filter_csr(pos.cpu().numpy(), "tail-batch")
+    trig = m._rank_rotation(DEV)
     torch.library.opcheck(torch.ops.kge.rank_filtered.default,
                           (ent.detach(), rel.detach(), None if mod is None else mod.detach(), pos,
-                           torch.from_numpy(off).to(DEV), torch.from_numpy(ids).to(DEV), "tail-batch", name, g, rng))
+                           torch.from_numpy(off).to(DEV), torch.from_numpy(ids).to(DEV), MODE_IDS["tail-batch"], mid,
+                           g, rng, 0, trig))
+    # the C++ op and the ctypes mirror give the same ranks (the op is what a libtorch caller binds)
+    r_op, t_op = torch.ops.kge.rank_filtered(ent.detach(), rel.detach(), None if mod is None else mod.detach(), pos,
+                                             torch.from_numpy(off).to(DEV), torch.from_numpy(ids).to(DEV),
+                                             MODE_IDS["tail-batch"], mid, g, rng, 0, trig)
+    r_py, t_py = m.rank_queries(pos.cpu().numpy(), pos.cpu().numpy().tolist(), "tail-batch")
+    assert np.array_equal(r_op.cpu().numpy(), r_py) and np.array_equal(t_op.cpu().numpy(), t_py)
 
 
 def test_compile_forward_fullgraph():
