@@ -33,7 +33,12 @@ namespace kge {
 // correctly rounded fp32 transcendentals (a double result rounded once)
 __device__ __forceinline__ float sin_rn(float x) { return (float)sin((double)x); }
 __device__ __forceinline__ float cos_rn(float x) { return (float)cos((double)x); }
-__device__ __forceinline__ float sqrt_rn(float x) { return __fsqrt_rn(x); }
+// correctly rounded sqrt, as ATen's: __builtin_sqrtf lowers to v_sqrt_f32 plus
+// the fma residual correction (the build keeps HIP's default correctly rounded
+// fp32 divide/sqrt).  NOT __fsqrt_rn: without OCML_BASIC_ROUNDED_OPERATIONS
+// that is the native ~1-ulp v_sqrt_f32 — which made FB15k RotatE ranks tie
+// (device) where the reference's differ by one ulp of the sum (2 / 256 queries).
+__device__ __forceinline__ float sqrt_rn(float x) { return __builtin_sqrtf(x); }
 
 // reference q for one element (model.py association).  RotatE: the rotation
 // (cos θ, sin θ) from the caller's table of the reference's own values when

@@ -88,6 +88,25 @@ def synth_tables(name, E, R, d, gamma, seed):
     return ent, rel, mod, rng
 
 
+def spawn_ranks(fn, args, nprocs):
+    """mp.spawn for ranks that share ONE GPU (the -m gpu multi-rank tests):
+    each rank limited to one HIP hardware queue.  With the default four per
+    process, five processes on one card (the pytest parent holds its own)
+    oversubscribe the card's hardware queue slots and the scheduler
+    time-slices them: the world-4 query-shipping case took 138 s instead of
+    5.4 s.  Product runs use one process per GPU."""
+    import torch.multiprocessing as mp
+    old = os.environ.get("GPU_MAX_HW_QUEUES")
+    os.environ["GPU_MAX_HW_QUEUES"] = "1"  # inherited by the spawned ranks only (read at their HIP init)
+    try:
+        mp.spawn(fn, args=args, nprocs=nprocs, join=True)
+    finally:
+        if old is None:
+            os.environ.pop("GPU_MAX_HW_QUEUES", None)
+        else:
+            os.environ["GPU_MAX_HW_QUEUES"] = old
+
+
 def score_tol(ref):
     """|Δ| ≤ 1e-4 · max(|s_ref|, 1) — the north-star fp32 score tolerance."""
     return 1e-4 * np.maximum(np.abs(ref), 1.0)

@@ -30,7 +30,7 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from conftest import score_tol
+from conftest import score_tol, spawn_ranks
 from knowledgegraphembedding_amd import KGEAdam, KGEModel, synth
 
 pytestmark = pytest.mark.gpu
@@ -109,7 +109,7 @@ def _worker(rank, world, port, exchange, out):
 @pytest.mark.parametrize("world,exchange", [(2, "owner"), (4, "owner"), (2, "factors")])
 def test_config4_shape_matches_one_process(world, exchange):
     out = mp.Manager().dict()
-    mp.spawn(_worker, args=(world, _free_port(), exchange, out), nprocs=world, join=True)
+    spawn_ranks(_worker, (world, _free_port(), exchange, out), world)
     model = _model()
     opt = KGEAdam([p for p in model.parameters() if p.requires_grad], lr=LR)
     it = iter(_batches(world, "cuda:0"))

@@ -17,6 +17,7 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
+from conftest import spawn_ranks
 from knowledgegraphembedding_amd import KGEAdam, KGEModel, synth
 
 pytestmark = pytest.mark.gpu
@@ -79,7 +80,7 @@ def _worker(rank, world, port, name, reg, uni, out):
 def test_factor_exchange_two_ranks_bitwise(name, reg, uni):
     world = 2
     out = mp.Manager().dict()
-    mp.spawn(_worker, args=(world, _free_port(), name, reg, uni, out), nprocs=world, join=True)
+    spawn_ranks(_worker, (world, _free_port(), name, reg, uni, out), world)
     model = _model(name)
     opt = KGEAdam([p for p in model.parameters() if p.requires_grad], lr=LR)
     it = iter(_batches("cuda:0"))

@@ -17,6 +17,7 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
+from conftest import spawn_ranks
 from knowledgegraphembedding_amd import KGEAdam, KGEModel, synth
 
 pytestmark = pytest.mark.gpu
@@ -88,7 +89,7 @@ def test_owner_exchange_bitwise(name, reg, uni, world, chunks, e):
     of 2 rows, rank 2 owns one row and rank 3 starts past the table (lo = 6),
     so its range is empty (the owner step clamps it)."""
     out = mp.Manager().dict()
-    mp.spawn(_worker, args=(world, _free_port(), name, reg, uni, chunks, e, out), nprocs=world, join=True)
+    spawn_ranks(_worker, (world, _free_port(), name, reg, uni, chunks, e, out), world)
     model = _model(name, e)
     opt = KGEAdam([p for p in model.parameters() if p.requires_grad], lr=LR)
     it = iter(_batches("cuda:0", e))

@@ -1,11 +1,13 @@
 """Pin the CPU oracle (oracle/kge_oracle.py) to the reference's own outputs
 (tests/golden/*.npz, made by tests/golden/make_golden.py from the imported
 reference).  CPU only."""
+import json
+
 import numpy as np
 import pytest
 import torch
 
-from conftest import dims, erange_of, synth_tables  # noqa: F401
+from conftest import GOLDEN, dims, erange_of, load_npz, synth_tables  # noqa: F401
 from knowledgegraphembedding_amd import synth
 from oracle import kge_oracle as O
 
@@ -149,3 +151,34 @@ def test_oracle_countries(g_countries, golden_info):
     np.testing.assert_allclose(y, g_countries["y_score"], rtol=1e-6, atol=1e-7)
     y_true = np.array([1 if c == t else 0 for _, _, t in test.tolist() for c in regions.tolist()])
     assert abs(average_precision_score(y_true, y) - g_countries["auc_pr"][0]) < 1e-9
+
+
+def test_reference_trig_fixture_against_host():
+    """tests/golden/rotate_trig.npz holds the reference's own cos / sin bits of
+    RotatE's relation phases (model.py:209-212) as an XOR against correctly
+    rounded values.  The XOR is sparse (the vector library is within an ulp),
+    and this host's torch.cos / torch.sin (ops.reference_rotation — what
+    KGEModel's ranking uses) give exactly the committed bits when the host's
+    CPU vector library matches the one the fixtures were made with."""
+    import torch
+    from conftest import erange_of
+    from knowledgegraphembedding_amd import ops, synth
+    g = load_npz("rotate_trig.npz")
+    info = {c["tag"]: c for c in json.load(open(GOLDEN / "golden.json"))["rotate_trig"]}
+    seeds = {"kg_small": (40, 31, 12.0), "kg_mid": (1500, 32, 12.0), "fb15k": (14951, 62, 24.0)}
+    differ = []
+    for tag, (E, seed, gamma) in seeds.items():
+        R, d = info[tag]["R"], info[tag]["d"]
+        rng = erange_of(gamma, d)
+        _, rel = synth.kge_tables(seed, E, R, 2 * d, d, rng)
+        ids = g[f"{tag}/rel_ids"]
+        xc, xs = g[f"{tag}/cos_xor"], g[f"{tag}/sin_xor"]
+        assert xc.shape == (len(ids), d) and 0 < (xc != 0).mean() < 0.1 and 0 < (xs != 0).mean() < 0.1
+        ph64 = (torch.from_numpy(rel) / (rng / ops.PI)).numpy().astype(np.float64)[ids]
+        ref_c = np.cos(ph64).astype(np.float32).view(np.uint32) ^ xc
+        ref_s = np.sin(ph64).astype(np.float32).view(np.uint32) ^ xs
+        host = ops.reference_rotation(torch.from_numpy(rel), rng).numpy()[ids]
+        differ.append(float((host[:, 0].view(np.uint32) != ref_c).mean() + (host[:, 1].view(np.uint32) != ref_s).mean()))
+    if any(differ):
+        pytest.skip(f"this host's CPU cos/sin differ from the reference's on {differ} of the fixture values "
+                    "(the GPU parity test ranks with the committed bits)")

@@ -9,6 +9,7 @@ import numpy as np
 import pytest
 import torch
 
+from conftest import spawn_ranks
 from knowledgegraphembedding_amd import run, synth
 
 pytestmark = pytest.mark.gpu
@@ -136,7 +137,7 @@ def test_run_data_parallel_host_loader_odd_train_set(tmp_path):
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
     s.close()
-    mp.spawn(_run_rowpart_worker, args=(2, port, data, save, ()), nprocs=2, join=True)
+    spawn_ranks(_run_rowpart_worker, (2, port, data, save, ()), 2)
     ckpt = torch.load(os.path.join(save, "checkpoint"), map_location="cpu", weights_only=True)
     assert ckpt["step"] == 29
     test1 = _metrics(os.path.join(save, "train.log"), "Test ")
@@ -157,7 +158,7 @@ def test_run_row_partition_query_shipping(tmp_path):
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
     s.close()
-    mp.spawn(_run_rowpart_worker, args=(2, port, data, save), nprocs=2, join=True)
+    spawn_ranks(_run_rowpart_worker, (2, port, data, save), 2)
     ckpt = torch.load(os.path.join(save, "checkpoint"), map_location="cpu", weights_only=True)
     assert ckpt["step"] == 29
     assert ckpt["model_state_dict"]["entity_embedding"].shape == (41, 32)

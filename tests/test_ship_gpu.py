@@ -17,6 +17,7 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
+from conftest import spawn_ranks
 from knowledgegraphembedding_amd import KGEAdam, KGEModel, synth
 
 pytestmark = pytest.mark.gpu
@@ -96,7 +97,7 @@ def test_query_shipping_matches_one_process(name, reg, uni, world, e, d, env):
     that are not float4-aligned (scalar-slot kernels, row-per-wave entity
     pass); KGE_ENT_SLICES=0: the row-per-wave entity pass on float4 rows."""
     out = mp.Manager().dict()
-    mp.spawn(_worker, args=(world, _free_port(), name, reg, uni, e, d, env, out), nprocs=world, join=True)
+    spawn_ranks(_worker, (world, _free_port(), name, reg, uni, e, d, env, out), world)
     model = _model(name, e, d)
     opt = KGEAdam([p for p in model.parameters() if p.requires_grad], lr=LR)
     it = iter(_batches("cuda:0", e))
