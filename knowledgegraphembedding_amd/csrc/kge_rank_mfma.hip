@@ -281,9 +281,9 @@ int launch_rank_mfma(int gather, const float* q, const float* ent, int64_t nq, i
   a.q = q; a.ent = ent; a.nq = nq; a.E = E; a.K = K; a.true_id = true_id; a.s_true = s_true;
   a.fbits = bits; a.W = (E + 31) / 32; a.gt = gt; a.win = win;
   const unsigned gy = (unsigned)((nq + BM - 1) / BM);
-  // 3 waves/SIMD (158 VGPRs, no spills); 4 fits only with 13 spilled VGPRs
-  // and measured 12 % slower
-  // buffer offsets are 32-bit: both operands must stay below 4 GB
+  // k_rank_mfma is __launch_bounds__(256, 4): ≤ 128 VGPRs (96 used) and 36 KB
+  // of LDS, 4 workgroups = 4 waves per SIMD (the LDS-DMA double buffer holds no
+  // staging registers); buffer offsets are 32-bit: both operands below 4 GB
   if ((uint64_t)E * K * 4 >= 0xFFFFFF00ull || (uint64_t)nq * K * 4 >= 0xFFFFFF00ull) return -1;
   if (gather) {
     hipLaunchKernelGGL((k_rank_mfma<true>), dim3(1, gy), dim3(256), 0, s, a);
