@@ -267,6 +267,8 @@ def main():
                     help="skip the per-stage HIP events (roofline then comes from the committed rocprof summary)")
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="fb15k")
     ap.add_argument("--no-rank", action="store_true", help="skip the config-3 ranking section (rank 0, 1 GPU)")
+    ap.add_argument("--hidden-dim", type=int, default=None,
+                    help="override the workload's hidden_dim (diagnostics; the headline is the workload's own)")
     ap.add_argument("--traffic-json", default=None,
                     help="rocprofv3 PMC summary (tools/pmc_traffic.py output) for roofline.traffic "
                          "(default: the committed profiles/pmc_traffic.json of this workload)")
@@ -274,6 +276,8 @@ def main():
     global E, R, D, B, NNEG
     wl = WORKLOADS[a.workload]
     E, R, D, B, NNEG = wl["E"], wl["R"], wl["D"], wl["B"], wl["NNEG"]
+    if a.hidden_dim:
+        D = a.hidden_dim
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))

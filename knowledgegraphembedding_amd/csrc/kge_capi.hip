@@ -347,6 +347,7 @@ int run_grad(const kge_model_desc* m, const Geom& geo, int mode, const int64_t* 
   ea.write_grad = write_grad;
   ea.nsl = nsl;
   ea.slice_w = nsl > 0 ? (geo.eg.S + nsl - 1) / nsl : 0;
+  ea.dma = (nsl > 0 && (double)B * Le * 4.0 < 2147483648.0 && env_int("KGE_ENT_DMA", 0) != 0) ? 1 : 0;
   ea.adam = adam_t(adam ? &adam->entity : nullptr);
   ea.adamk = ak;
   ea.rel = rl;
@@ -752,6 +753,7 @@ int kge_ship_step(const kge_model_desc* m, int32_t mode, const kge_ship_desc* sh
   ea.write_grad = (!adam || adam->write_grad) ? 1 : 0;
   ea.nsl = nsl;
   ea.slice_w = nsl > 0 ? (geo.eg.S + nsl - 1) / nsl : 0;
+  ea.dma = (nsl > 0 && (double)B * Le * 4.0 < 2147483648.0 && env_int("KGE_ENT_DMA", 0) != 0) ? 1 : 0;
   ea.adam = adam_t(adam ? &adam->entity : nullptr);
   ea.adamk = ak;
   ea.B = B;

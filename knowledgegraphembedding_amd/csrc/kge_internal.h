@@ -119,6 +119,7 @@ struct EntArgs {
   int64_t B;            // batch rows (the q buffer's height)
   int nsl;              // > 0: column-sliced pass k_entity_sl with nsl slices of slice_w slots (VEC = 4)
   int slice_w;
+  int dma;              // k_entity_sl stages the q slices by LDS-DMA (needs B·Le·4 < 2^31)
   AdamT adam;           // fused optimizer step (adam.p == null: none)
   AdamK adamk;
   RelArgs rel;          // rel_blocks > 0: trailing blocks of k_entity_sl run the relation pass

@@ -487,7 +487,8 @@ def test_config2_full_size_properties():
                                       ("DistMult", 52, 700)])
 def test_entity_pass_column_slices_bitwise(name, d, B, monkeypatch):
     """The column-sliced entity pass (k_entity_sl with nsl = 1, 2, 4, 8
-    slices — the count is picked per shape) and the row-per-wave pass
+    slices — the count is picked per shape — with the q slices loaded into
+    registers or staged by LDS-DMA) and the row-per-wave pass
     (k_entity, the path for rows that are not float4-aligned; KGE_ENT_SLICES=0
     forces it here) apply the same per-element arithmetic in the same
     occurrence order: identical gradients and fused Adam updates, bit for bit
@@ -498,9 +499,11 @@ def test_entity_pass_column_slices_bitwise(name, d, B, monkeypatch):
     pos, neg, w = synth.kge_batch(88, B, n, E, R)
     P, N, W = torch.from_numpy(pos).to(DEV), torch.from_numpy(neg).to(DEV), torch.from_numpy(w).to(DEV)
     out = {}
-    variants = ("0", "1", "2", "4", "8") if d == 200 else ("0", "-1")
+    # "<slices>d": the same slices with the q slices staged by LDS-DMA (KGE_ENT_DMA=1)
+    variants = ("0", "1", "2", "4", "8", "1d", "4d", "8d") if d == 200 else ("0", "-1", "-1d")
     for nsl in variants:
-        monkeypatch.setenv("KGE_ENT_SLICES", nsl)
+        monkeypatch.setenv("KGE_ENT_SLICES", nsl.rstrip("d"))
+        monkeypatch.setenv("KGE_ENT_DMA", "1" if nsl.endswith("d") else "0")
         m, *_ = build_model(name, E, R, d, 12.0, 5)
         opt = KGEAdam([p for p in m.parameters() if p.requires_grad], lr=1e-3)
         res = []
