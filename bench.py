@@ -217,13 +217,16 @@ def cpu_baseline(model_cpu_state, budget_s: float = 12.0, b: int = 32):
 
 def rank_section(dev, reps: int = 3) -> dict:
     """BASELINE config 3, measured live beside the training metric: filtered
-    ranking (KGEModel.rank_queries_both → kge_rank_filtered: MFMA tile + near-tie
-    refinement in the reference's order) of all 3134 wn18rr-shape test triples
-    in both directions (6268 queries, E=40943, d=500) against a synthetic
-    filter graph of wn18rr's 93,003 true triples (tools/bench_rank.py, same
-    data).  `tflops` = 2·queries·E·K / wall time of the whole pass (host CSR,
-    bitmap, window, MFMA tile, refinement, read-back): a lower bound on the
-    MFMA tile's own rate (its rocprofv3 time: profiles/r02/rank_*)."""
+    ranking (KGEModel.rank_queries_both → kge_rank_filtered: split-bf16 MFMA
+    tile + near-tie refinement in the reference's order) of all 3134
+    wn18rr-shape test triples in both directions (6268 queries, E=40943, d=500)
+    against a synthetic filter graph of wn18rr's 93,003 true triples
+    (tools/bench_rank.py, same data).  `tflops` = 2·queries·E·K / wall time of
+    the whole pass (host CSR, bitmap, operand split, window, MFMA tile,
+    refinement, read-back) in fp32-product terms; the tile computes each fp32
+    product as four bf16 MFMA products (x = x_hi + x_lo), so `frac` against
+    the fp32 MFMA peak can pass 1 and `bf16_frac` = 4·flops / time / 2.5 PF is
+    the matrix cores' own share (tile alone: profiles/r03/rank/)."""
     import numpy as np
     from knowledgegraphembedding_amd import synth
     from knowledgegraphembedding_amd.filters import FilterIndex
@@ -250,6 +253,8 @@ def rank_section(dev, reps: int = 3) -> dict:
         flops = 2.0 * 2 * ntest * Ew * K
         out[name] = {"ms": best * 1e3, "queries_per_s": 2 * ntest / best, "tflops": flops / best / 1e12,
                      "fp32_mfma_peak_tflops": 157.3, "frac": flops / best / 1e12 / 157.3,
+                     "bf16_frac": 4 * flops / best / 1e12 / 2500.0,
+                     "path": "split-bf16 MFMA tile (4 bf16 products per fp32 product) + reference-order refinement",
                      "mrr": float(np.mean(1.0 / np.concatenate([rh, rt])))}
         del m
     torch.cuda.empty_cache()

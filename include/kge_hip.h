@@ -407,9 +407,10 @@ int kge_rank_filtered(const kge_model_desc *m, int32_t mode, const int64_t *quer
                       int32_t *ties_out, void *workspace, size_t workspace_bytes, int32_t *err_flag,
                       void *stream);
 /*
- * The same with the fast pass chosen (path: 0 auto, 1 MFMA tile — DistMult /
- * ComplEx with float4-aligned rows, 2 register tile — reduction length % 4 ==
- * 0, 3 wave scan; KGE_ERR_ARG if the rows do not suit the requested path) and
+ * The same with the fast pass chosen (path: 0 auto, 1 split-bf16 MFMA tile —
+ * DistMult / ComplEx, 4 fp32 MFMA tile — DistMult / ComplEx with float4-aligned
+ * rows, 2 register tile — reduction length % 4 == 0, 3 wave scan; KGE_ERR_ARG
+ * if the rows do not suit the requested path) and
  * listed_out [nq] int32 (nullable): near-ties re-scored per query (above the
  * 1024-per-query list capacity the query is rescanned exactly).  Every path
  * returns the same ranks and ties.

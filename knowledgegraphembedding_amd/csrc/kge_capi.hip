@@ -61,25 +61,28 @@ int check_model(const kge_model_desc* m, Geom* g) {
   return KGE_OK;
 }
 
-// Fast counting pass of the filtered ranking (path 0 = auto): the fp32 MFMA
-// tile for DistMult / ComplEx with float4-aligned rows, the register tile for
+// Fast counting pass of the filtered ranking (path 0 = auto): the split-bf16
+// MFMA tile for DistMult / ComplEx (path 1; the fp32 MFMA tile, path 4, when
+// the split operands would pass 32-bit buffer offsets), the register tile for
 // the others when the reduction length is a multiple of 4, the wave scan
 // otherwise.  Every path ends in the same reference-order refinement, so all
 // give the same ranks.
-enum RankPath : int { RP_AUTO = 0, RP_MFMA = 1, RP_TILE = 2, RP_SCAN = 3 };
+enum RankPath : int { RP_AUTO = 0, RP_MFMA = 1, RP_TILE = 2, RP_SCAN = 3, RP_MFMA32 = 4 };
 int rank_path(const kge_model_desc* m, int requested) {
   const bool bil = (m->model == KGE_DISTMULT || m->model == KGE_COMPLEX);
   const bool cplx = (m->model == KGE_ROTATE || m->model == KGE_COMPLEX);
   const int K = cplx ? m->entity_dim / 2 : m->entity_dim;
   const bool al = aligned16(m->entity_embedding);
-  // (the MFMA tile addresses the table through 32-bit buffer offsets)
+  // (the MFMA tiles address their operands through 32-bit buffer offsets)
+  const bool x_ok = bil && (uint64_t)xsplit_elems(m->nentity, m->entity_dim) * 2u < 0x7FFFFFF0ull;
   const bool mfma_ok = bil && (m->entity_dim % 4 == 0) && al &&
                        (uint64_t)m->nentity * (uint64_t)m->entity_dim * 4u < 0xFFFFFF00ull;
   const bool tile_ok = (K % 4 == 0) && al;
-  if (requested == RP_MFMA) return mfma_ok ? RP_MFMA : -1;
+  if (requested == RP_MFMA) return x_ok ? RP_MFMA : -1;
+  if (requested == RP_MFMA32) return mfma_ok ? RP_MFMA32 : -1;
   if (requested == RP_TILE) return tile_ok ? RP_TILE : -1;
   if (requested == RP_SCAN) return RP_SCAN;
-  return mfma_ok ? RP_MFMA : (tile_ok ? RP_TILE : RP_SCAN);
+  return x_ok ? RP_MFMA : mfma_ok ? RP_MFMA32 : (tile_ok ? RP_TILE : RP_SCAN);
 }
 constexpr int RANK_CAP = 1024;  // listed near-ties per query before the exact rescan takes over
 
@@ -869,6 +872,7 @@ struct RankWs {
   int64_t* true_id;
   int32_t *gt, *eq, *gtx, *eqx, *ucnt, *ulist;
   uint32_t* bits;
+  uint16_t *qs, *es;  // split-bf16 operands (DistMult / ComplEx)
 };
 RankWs carve_rank(void* ws, const kge_model_desc* m, int64_t nq, size_t* bytes) {
   Carver c(ws);
@@ -887,6 +891,9 @@ RankWs carve_rank(void* ws, const kge_model_desc* m, int64_t nq, size_t* bytes) 
   w.ucnt = w.gt ? w.gt + 4 * nq : nullptr;
   w.ulist = c.take<int32_t>(nq * (int64_t)RANK_CAP);
   w.bits = c.take<uint32_t>(nq * ((m->nentity + 31) / 32));
+  const bool bil = (m->model == KGE_DISTMULT || m->model == KGE_COMPLEX);
+  w.qs = c.take<uint16_t>(bil ? xsplit_elems(nq, m->entity_dim) : 0);
+  w.es = c.take<uint16_t>(bil ? xsplit_elems(m->nentity, m->entity_dim) : 0);
   *bytes = c.off + 256;
   return w;
 }
@@ -910,7 +917,7 @@ int kge_rank_filtered_ex(const kge_model_desc* m, int32_t mode, const int64_t* q
   if (st) return st;
   if (mode != KGE_HEAD_BATCH && mode != KGE_TAIL_BATCH) return KGE_ERR_MODE;
   if (!queries || !filt_off || !ranks_out || !err_flag || nq < 0) return KGE_ERR_ARG;
-  if (path < RP_AUTO || path > RP_SCAN) return KGE_ERR_ARG;
+  if (path < RP_AUTO || path > RP_MFMA32) return KGE_ERR_ARG;
   if (nq == 0) return KGE_OK;
   if (nq > 65535) return KGE_ERR_DIM;  // the bitmap launch puts queries on grid.y
   const int rp = rank_path(m, path);
@@ -957,7 +964,13 @@ int kge_rank_filtered_ex(const kge_model_desc* m, int32_t mode, const int64_t* q
   ta.nq = nq; ta.E = m->nentity; ta.Le = m->entity_dim; ta.K = K;
   ta.c = a.c; ta.true_id = w.true_id; ta.s_true = w.s_true;
   ta.fbits = w.bits; ta.W = a.W; ta.gt = w.gt; ta.win = win;
-  if (rp == RP_MFMA)
+  if (rp == RP_MFMA) {
+    st = launch_status(launch_split_bf16(w.q, nq, m->entity_dim, w.qs, s));
+    if (!st) st = launch_status(launch_split_bf16(m->entity_embedding, m->nentity, m->entity_dim, w.es, s));
+    if (!st)
+      st = launch_status(launch_rank_mfma_x(1, w.qs, w.es, nq, m->nentity, m->entity_dim, w.true_id, w.s_true,
+                                            w.bits, w.gt, win, s));
+  } else if (rp == RP_MFMA32)
     st = launch_status(launch_rank_mfma(1, w.q, m->entity_embedding, nq, m->nentity, m->entity_dim, w.true_id,
                                         w.s_true, w.bits, w.gt, win, s));
   else if (rp == RP_TILE)
@@ -974,10 +987,16 @@ int kge_rank_filtered_ex(const kge_model_desc* m, int32_t mode, const int64_t* q
   ra.ucnt = w.ucnt; ra.ulist = w.ulist; ra.cap = RANK_CAP;
   ra.fbits = w.bits; ra.W = a.W; ra.gt = w.gt; ra.eq = w.eq; ra.gtx = w.gtx; ra.eqx = w.eqx; ra.err = err_flag;
   ra.trig = trig;
+  // the split-bf16 tile's error bound in units of u·‖q‖·max‖e‖ (kge_rank_mfma.hip)
+  const int64_t xns = xsplit_nslab(m->entity_dim);
+  ra.fast_u = (rp == RP_MFMA) ? (float)(546.0 + 1.02 * xns + 0.05 * xns * 16) : 0.f;
   st = launch_status(ops.rank_ref(mode, 0, ra, s));
   if (st) return st;
   // 5. fast counting pass: clear cases counted, near-ties listed
   if (rp == RP_MFMA) {
+    st = launch_status(launch_rank_mfma_x(0, w.qs, w.es, nq, m->nentity, m->entity_dim, w.true_id, w.s_true,
+                                          w.bits, w.gt, win, s));
+  } else if (rp == RP_MFMA32) {
     st = launch_status(launch_rank_mfma(0, w.q, m->entity_embedding, nq, m->nentity, m->entity_dim, w.true_id,
                                         w.s_true, w.bits, w.gt, win, s));
   } else if (rp == RP_TILE) {

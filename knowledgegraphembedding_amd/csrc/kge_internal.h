@@ -199,6 +199,8 @@ struct RefArgs {
   int32_t* eqx;
   int32_t* err;
   const float* trig;       // RotatE: [R, 2, Lr] reference cos | sin of the phases, or null
+  float fast_u;            // > 0: the fast pass's error bound in u·‖q‖·max‖e‖ (split-bf16 tile)
+  int ref_slots;           // k_rank_refine: half-waves with an LDS row slot (set by its launcher)
 };
 
 // Register-tiled filtered ranking (kge_kernels.inc, k_rank_tile): 64 queries ×

@@ -134,15 +134,23 @@ __global__ __launch_bounds__(256, 4) void k_rank_mfma(MfmaArgs a) {
 
   const int kh = lane >> 5, li = lane & 31;
   const int nslab = (a.K + BK2 - 1) / BK2;
+  // a wave whose 64 queries (or 64 candidates) all lie past nq (E) still
+  // loads its share of every slab, but issues no MFMA: its SIMD's matrix core
+  // goes to the co-resident workgroups (wn = 1 of the last query row of
+  // blocks for wn18rr's 3134 queries: 2 % of the launch)
+  const bool live = q0 + wn * 64 < a.nq && (GATHER || e0 + wm * 64 < a.E);
   issue(0, 0);
   for (int s = 0; s < nslab; ++s) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA of slab s has landed
     __syncthreads();                                   // ... every wave's; slab s-1's reads are done
     if (s + 1 < nslab) issue((s + 1) * BK2, (s + 1) & 1);
+    if (!live) continue;
     const float* As = smem + (s & 1) * STAGE2;
     const float* Bs = As + 128 * BK2;
+    const int kv = a.K - s * BK2;  // k past the reduction length read as 0: skip whole 8-k groups of them
 #pragma unroll
     for (int g = 0; g < BK2 / 8; ++g) {
+      if (g > 0 && 8 * g >= kv) break;
       float4 e4[2], q4[2];
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
@@ -253,6 +261,269 @@ __global__ __launch_bounds__(256) void k_rank_emit(EmitArgs a) {
   if (a.listed) a.listed[q] = ok ? a.ucnt[q] : 0;
 }
 
+
+// --------------------------------------------------------------------------
+// Split-bf16 MFMA tile (path "mfma", the default for DistMult / ComplEx).
+//
+// fp32 MFMA runs at 1/16 of the bf16 rate on gfx950 (v_mfma_f32_32x32x2_f32:
+// 64 cycles per 4096 flop; v_mfma_f32_32x32x16_bf16: 32 cycles per 32768).
+// The fast pass only has to place each candidate on the right side of s_true
+// up to the near-tie window — the window's candidates are re-scored in the
+// reference's fp32 order anyway — so it may compute in any precision whose
+// error it bounds.  Each operand x is split as x = x_hi + x_lo + r with
+// x_hi = bf16(x), x_lo = bf16(x − x_hi) (both RNE, |r| ≤ 2^-16 |x|), and
+//   s ≈ Σ_slab fl(Σ_16 e_hi q_hi)  +  Σ_k (e_hi q_lo + e_lo q_hi + e_lo q_lo)
+// (bf16 × bf16 products are exact in fp32).  The hi·hi part of each 16-k
+// slab comes from an MFMA with a zero accumulator and is added to an fp32
+// running sum by v_add (rounded once per slab); the three small products
+// chain in a second accumulator.  Error per score, P = Σ|q_k||e_k| ≤ ‖q‖‖e‖:
+//   splitting 512.1·u·P, hi·hi MFMAs 32.3·u·P (2u per internal add, any
+//   order), running sum 1.02·nslab·u·P, correction chain 0.0472·Kp·u·P
+//   (3 Kp terms of total size ≤ 2^-7·P), final add 1.01·u·P
+// → (546 + 1.02·nslab + 0.05·Kp)·u·P (k_rank_window, xsplit = 1), about the
+// fp32 tile's K·u for K = 500 and below it for larger K.
+//
+// Operands are split once per call into a tile-linear layout
+// [row block of 128][16-k slab][hi | lo][128 rows][16 k] bf16 (k_split_bf16),
+// so each slab of a 128-row block is 8 KB contiguous: four 1 KB LDS-DMA
+// instructions per piece, and the fragment reads (row r, k-half h at
+// r·32 + h·16 bytes) are conflict-free.  Rows past nq / E and k ≥ K are
+// zeros in the split buffers.  256 threads as 2×2 waves of 64×64 (2×2 MFMA
+// tiles), 4-stage LDS ring (64 KB) with 3 slabs in flight, 2 workgroups per CU.
+typedef short bf16x8 __attribute__((ext_vector_type(8)));
+constexpr int XS_BK = 16;                   // k per slab = one 32x32x16 MFMA step
+constexpr int XS_PIECE = 128 * XS_BK;       // bf16 per (row block, slab, hi|lo) = 4 KB
+constexpr int XS_NST = 4;                   // LDS ring stages
+constexpr uint32_t XS_OOB = 0x7FFFFFF0u;
+
+__device__ __forceinline__ uint32_t bf16_rne(float x) {
+  const uint32_t b = __float_as_uint(x);
+  if (x != x) return 0x7FC0u;
+  return (b + 0x7FFFu + ((b >> 16) & 1u)) >> 16;
+}
+
+// dst[(rb·nslab + s)·2 + piece][rr][kk] for rows < rows, k < K (zeros elsewhere).
+// A wave takes 8 rows × 64 k: lane (r8, g8) = (lane >> 3, lane & 7) converts
+// the 8 floats k = 64·chunk + 8·g8 … of row 8·group + r8, so each row is read
+// as 256 contiguous bytes and, per slab, the 8 rows' hi (lo) pieces are
+// written as 256 contiguous bytes.
+__global__ __launch_bounds__(256) void k_split_bf16(const float* __restrict__ src, int64_t rows, int K, int nslab,
+                                                    int64_t nrb, uint16_t* __restrict__ dst) {
+  const int64_t wg = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
+  const int nc = (nslab * XS_BK + 63) / 64;  // 64-k chunks per row
+  const int64_t rg = wg / nc;
+  if (rg >= nrb * 16) return;
+  const int kg = (int)(wg % nc) * 8 + (lane & 7);  // 8-k group
+  if (kg >= nslab * 2) return;
+  const int64_t row = rg * 8 + (lane >> 3);
+  const int k0 = kg * 8;
+  float x[8];
+  const float* p = src + row * K + k0;
+  if (row < rows && k0 + 8 <= K && ((K & 3) == 0) && ((((uintptr_t)src) & 15) == 0)) {
+    const float4 a = reinterpret_cast<const float4*>(p)[0], b = reinterpret_cast<const float4*>(p)[1];
+    x[0] = a.x; x[1] = a.y; x[2] = a.z; x[3] = a.w; x[4] = b.x; x[5] = b.y; x[6] = b.z; x[7] = b.w;
+  } else {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) x[j] = (row < rows && k0 + j < K) ? p[j] : 0.f;
+  }
+  uint32_t hi[8], lo[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    hi[j] = bf16_rne(x[j]);
+    lo[j] = bf16_rne(x[j] - __uint_as_float(hi[j] << 16));  // exact difference
+  }
+  const uint4 vh = {hi[0] | (hi[1] << 16), hi[2] | (hi[3] << 16), hi[4] | (hi[5] << 16), hi[6] | (hi[7] << 16)};
+  const uint4 vl = {lo[0] | (lo[1] << 16), lo[2] | (lo[3] << 16), lo[4] | (lo[5] << 16), lo[6] | (lo[7] << 16)};
+  const int64_t rb = row >> 7;
+  uint16_t* o = dst + ((rb * nslab + (kg >> 1)) * 2) * XS_PIECE + (row & 127) * XS_BK + (kg & 1) * 8;
+  *reinterpret_cast<uint4*>(o) = vh;
+  *reinterpret_cast<uint4*>(o + XS_PIECE) = vl;
+}
+
+struct XArgs {
+  const uint16_t* qs;  // split q
+  const uint16_t* es;  // split entity table
+  uint32_t qs_bytes, es_bytes;
+  int64_t nq, E;
+  int nslab;
+  const int64_t* true_id;
+  float* s_true;
+  const uint32_t* fbits;
+  int64_t W;
+  int32_t* gt;
+  RankWin win;
+};
+
+template <bool GATHER>
+__global__ __launch_bounds__(256, 2) void k_rank_mfma_x(XArgs a) {
+  // one LDS array: [XS_NST stages][E_hi | E_lo | Q_hi | Q_lo] then arow/brow, sts, sdl, cgt
+  __shared__ __attribute__((aligned(16))) uint16_t smem[XS_NST * 4 * XS_PIECE + 128 * 4 * 2 + 128 * 2 * 2 + 128 * 2 * 3];
+  int64_t* arow = reinterpret_cast<int64_t*>(smem + XS_NST * 4 * XS_PIECE);
+  int64_t* brow = arow + 128;
+  float* sts = reinterpret_cast<float*>(brow + 128);
+  float* sdl = sts + 128;
+  int32_t* cgt = reinterpret_cast<int32_t*>(sdl + 128);
+  const int t = threadIdx.x, lane = t & 63, w = wave_id();
+  const int wm = w >> 1, wn = w & 1;
+  const int64_t q0 = (int64_t)blockIdx.y * BM;
+  const int64_t e0 = (int64_t)blockIdx.x * BN;
+  if (t < 128) {
+    const int64_t q = q0 + t;
+    arow[t] = (q < a.nq) ? q : -1;
+    const int64_t tid_ = (q < a.nq) ? a.true_id[q] : -1;
+    if (GATHER) {
+      brow[t] = (tid_ >= 0 && tid_ < a.E) ? tid_ : -1;
+    } else {
+      sts[t] = (q < a.nq) ? a.s_true[q] : 0.f;
+      sdl[t] = (q < a.nq) ? a.win.delta[q] : 0.f;
+    }
+    cgt[t] = 0;
+  }
+  __syncthreads();
+
+  const auto rq = buf_rsrc(a.qs, a.qs_bytes);
+  const auto re = buf_rsrc(a.es, a.es_bytes);
+  const int nslab = a.nslab;
+  // wave w moves piece w of every slab: 0 E_hi, 1 E_lo, 2 Q_hi, 3 Q_lo (4 × 1 KB)
+  const bool wq = w >= 2;
+  const int piece = w & 1;
+  int64_t grow[4];  // GATHER, E pieces: this lane's source row of chunk c (row c·32 + lane/2)
+#pragma unroll
+  for (int c = 0; c < 4; ++c) grow[c] = (GATHER && !wq) ? brow[c * 32 + (lane >> 1)] : 0;
+  const int64_t rb_tile = wq ? (int64_t)blockIdx.y : (int64_t)blockIdx.x;
+  auto issue = [&](int sl, int st) {
+    uint16_t* base = smem + (st * 4 + w) * XS_PIECE;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      uint32_t off;
+      if (GATHER && !wq) {
+        const int64_t r = grow[c];
+        off = (r >= 0) ? (uint32_t)((((r >> 7) * nslab + sl) * 2 + piece) * (2 * XS_PIECE) + (r & 127) * 32 +
+                                    (lane & 1) * 16)
+                       : XS_OOB;
+      } else {
+        off = (uint32_t)(((rb_tile * nslab + sl) * 2 + piece) * (2 * XS_PIECE) + c * 1024 + lane * 16);
+      }
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(wq ? rq : re,
+                                               (__attribute__((address_space(3))) void*)(base + c * 512), 16, off,
+                                               0, 0, 0);
+    }
+  };
+  // DMAs issued after slab sl's, when sl is waited for: those of the next
+  // min(2, nslab − 1 − sl) slabs, 4 instructions each (vmcnt counts in order)
+  auto wait_slab = [&](int sl) {
+    const int after = nslab - 1 - sl;
+    if (after >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if (after == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  };
+
+  f32x16 run[2][2], cor[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) run[i][j][r] = cor[i][j][r] = 0.f;
+  const f32x16 zero = {};
+
+  const int kh = lane >> 5, li = lane & 31;
+  const bool live = q0 + wn * 64 < a.nq && (GATHER || e0 + wm * 64 < a.E);
+#pragma unroll
+  for (int p = 0; p < XS_NST - 1; ++p)
+    if (p < nslab) issue(p, p);
+  for (int sl = 0; sl < nslab; ++sl) {
+    wait_slab(sl);                // this wave's DMA of slab sl has landed
+    __builtin_amdgcn_s_barrier();  // ... every wave's; slab sl-1's reads are done (no fence: the
+                                   // vmcnt above covers the DMA, __syncthreads' would be vmcnt(0))
+    if (sl + XS_NST - 1 < nslab) issue(sl + XS_NST - 1, (sl + XS_NST - 1) % XS_NST);
+    if (!live) continue;
+    const uint16_t* Eh = smem + (sl % XS_NST) * 4 * XS_PIECE;
+    const uint16_t* El = Eh + XS_PIECE;
+    const uint16_t* Qh = Eh + 2 * XS_PIECE;
+    const uint16_t* Ql = Eh + 3 * XS_PIECE;
+    bf16x8 eh[2], el[2], qh[2], ql[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int row = wm * 64 + i * 32 + li;
+      eh[i] = *reinterpret_cast<const bf16x8*>(Eh + row * XS_BK + kh * 8);
+      el[i] = *reinterpret_cast<const bf16x8*>(El + row * XS_BK + kh * 8);
+    }
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int row = wn * 64 + j * 32 + li;
+      qh[j] = *reinterpret_cast<const bf16x8*>(Qh + row * XS_BK + kh * 8);
+      ql[j] = *reinterpret_cast<const bf16x8*>(Ql + row * XS_BK + kh * 8);
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const f32x16 m = __builtin_amdgcn_mfma_f32_32x32x16_bf16(eh[i], qh[j], zero, 0, 0, 0);
+        run[i][j] += m;
+        cor[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(eh[i], ql[j], cor[i][j], 0, 0, 0);
+        cor[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(el[i], qh[j], cor[i][j], 0, 0, 0);
+        cor[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(el[i], ql[j], cor[i][j], 0, 0, 0);
+      }
+  }
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = run[i][j] + cor[i][j];
+
+  // C/D layout as the fp32 tile: col (query) = lane & 31, row (candidate) = (reg & 3) + 8·(reg >> 2) + 4·(lane >> 5)
+  if (GATHER) {
+    if (wm != wn || kh != ((li >> 2) & 1)) return;
+    const int rd = 4 * (li >> 3) + (li & 3);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int n = wn * 64 + i * 32 + li;
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        if (r == rd && arow[n] >= 0) a.s_true[q0 + n] = acc[i][i][r];
+    }
+    return;
+  }
+  const int64_t wbase = e0 >> 5;
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int n = wn * 64 + j * 32 + li;
+    const int64_t q = arow[n];
+    const float st = sts[n], dlt = sdl[n];
+    uint32_t ex[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int64_t widx = wbase + wm * 2 + i;
+      const int64_t cbase = e0 + wm * 64 + i * 32;
+      uint32_t word = (q >= 0 && widx < a.W) ? a.fbits[q * a.W + widx] : ~0u;
+      const int64_t valid = a.E - cbase;
+      if (valid < 32) word |= (valid <= 0) ? ~0u : (~0u << valid);
+      ex[i] = word;
+    }
+    int g = 0;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int mloc = (r & 3) + 8 * (r >> 2) + 4 * kh;
+        const bool ok = ((ex[i] >> mloc) & 1u) == 0u;
+        const float sc = acc[i][j][r];
+        const float diff = sc - st;
+        g += (ok && diff > dlt) ? 1 : 0;
+        if (ok && !(diff > dlt) && diff >= -dlt) {
+          const int idx = atomicAdd(&a.win.ucnt[q], 1);
+          if (idx < a.win.cap) a.win.ulist[q * (int64_t)a.win.cap + idx] = (int32_t)(e0 + wm * 64 + i * 32 + mloc);
+        }
+      }
+    g += __shfl_xor(g, 32);
+    if (kh == 0 && q >= 0 && g) atomicAdd(&cgt[n], g);
+  }
+  __syncthreads();
+  if (t < 128 && arow[t] >= 0 && cgt[t]) atomicAdd(&a.gt[q0 + t], cgt[t]);
+}
+
 }  // namespace
 
 int launch_filter_bits(const int64_t* filt_off, const int64_t* filt_ids, const int64_t* true_id, int64_t nq,
@@ -294,38 +565,84 @@ int launch_rank_mfma(int gather, const float* q, const float* ent, int64_t nq, i
   return (int)hipGetLastError();
 }
 
+// split-bf16 tile: buffer sizes and launchers (path "mfma")
+int64_t xsplit_nslab(int K) { return (K + XS_BK - 1) / XS_BK; }
+int64_t xsplit_elems(int64_t rows, int K) { return ((rows + 127) / 128) * 128 * xsplit_nslab(K) * XS_BK * 2; }
+
+int launch_split_bf16(const float* src, int64_t rows, int K, uint16_t* dst, hipStream_t s) {
+  const int64_t nrb = (rows + 127) / 128, nslab = xsplit_nslab(K);
+  const int64_t waves = nrb * 16 * ((nslab * XS_BK + 63) / 64);  // 8 rows × 64 k each
+  hipLaunchKernelGGL(k_split_bf16, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s, src, rows, K, (int)nslab,
+                     nrb, dst);
+  return (int)hipGetLastError();
+}
+
+int launch_rank_mfma_x(int gather, const uint16_t* qs, const uint16_t* es, int64_t nq, int64_t E, int K,
+                       const int64_t* true_id, float* s_true, const uint32_t* bits, int32_t* gt, const RankWin& win,
+                       hipStream_t s) {
+  XArgs a;
+  a.qs = qs; a.es = es; a.nq = nq; a.E = E; a.nslab = (int)xsplit_nslab(K);
+  const uint64_t qb = (uint64_t)xsplit_elems(nq, K) * 2u, eb = (uint64_t)xsplit_elems(E, K) * 2u;
+  if (qb >= XS_OOB || eb >= XS_OOB) return -1;  // 32-bit buffer offsets, XS_OOB reads zeros
+  a.qs_bytes = (uint32_t)qb; a.es_bytes = (uint32_t)eb;
+  a.true_id = true_id; a.s_true = s_true; a.fbits = bits; a.W = (E + 31) / 32; a.gt = gt; a.win = win;
+  const unsigned gy = (unsigned)((nq + BM - 1) / BM);
+  // __launch_bounds__(256, 2): 64 KB ring + 4.4 KB, ≤ 256 VGPRs — 2 workgroups = 2 waves per SIMD
+  if (gather) {
+    hipLaunchKernelGGL((k_rank_mfma_x<true>), dim3(1, gy), dim3(256), 0, s, a);
+  } else {
+    const dim3 gs((unsigned)((E + BN - 1) / BN), gy);
+    hipLaunchKernelGGL((k_rank_mfma_x<false>), gs, dim3(256), 0, s, a);
+  }
+  return (int)hipGetLastError();
+}
+
 // Entity-table statistics for the ranking windows: stats[0] = max row L2
 // norm, stats[1] = max |x| (non-negative floats order like their bit
-// patterns, so an integer atomicMax is exact).  One wave per row, rows
-// strided over a bounded grid; the block's four waves combine in LDS and the
-// block issues one atomic per statistic (an atomic per row on the same two
-// words serialised: 0.93 ms for wn18rr's 40,943 rows).
+// patterns, so an integer atomicMax is exact).  Each wave takes TS_ROWS rows
+// at a time with their loads interleaved (TS_ROWS float4s in flight per lane;
+// one row per wave at a time left the pass latency-bound: 0.24 ms for
+// wn18rr's 40,943 × 500 table, r02), rows strided over a bounded grid; the
+// block's four waves combine in LDS and the block issues one atomic per
+// statistic (an atomic per row on the same two words serialised: 0.93 ms).
+constexpr int TS_ROWS = 4;
 __global__ __launch_bounds__(256) void k_table_stats(const float* __restrict__ ent, int64_t E, int Le,
                                                      float* stats) {
   __shared__ float red[2][4];
   const int lane = threadIdx.x & 63, w = wave_id();
+  const bool vec4 = (Le & 3) == 0 && (((uintptr_t)ent) & 15) == 0;
+  const int nk = vec4 ? Le / 4 : Le;
   float bn = 0.f, bm = 0.f;
-  for (int64_t e = (int64_t)blockIdx.x * 4 + w; e < E; e += (int64_t)gridDim.x * 4) {
-    const float* row = ent + e * Le;
-    float s2 = 0.f, mx = 0.f;
-    if ((Le & 3) == 0 && (((uintptr_t)ent) & 15) == 0) {  // float4 rows
-      for (int k = lane; k < Le / 4; k += 64) {
-        const float4 v = reinterpret_cast<const float4*>(row)[k];
-        s2 += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
-        mx = fmaxf(mx, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
-      }
-    } else {
-      for (int k = lane; k < Le; k += 64) {
-        const float v = row[k];
-        s2 += v * v;
-        mx = fmaxf(mx, fabsf(v));
+  const int64_t stride = (int64_t)gridDim.x * 4 * TS_ROWS;
+  for (int64_t e0 = ((int64_t)blockIdx.x * 4 + w) * TS_ROWS; e0 < E; e0 += stride) {
+    float s2[TS_ROWS], mx[TS_ROWS];
+#pragma unroll
+    for (int r = 0; r < TS_ROWS; ++r) s2[r] = mx[r] = 0.f;
+    for (int k = lane; k < nk; k += 64) {
+#pragma unroll
+      for (int r = 0; r < TS_ROWS; ++r) {
+        if (e0 + r >= E) continue;
+        const float* row = ent + (e0 + r) * Le;
+        if (vec4) {
+          const float4 v = reinterpret_cast<const float4*>(row)[k];
+          s2[r] += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+          mx[r] = fmaxf(mx[r], fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+        } else {
+          const float v = row[k];
+          s2[r] += v * v;
+          mx[r] = fmaxf(mx[r], fabsf(v));
+        }
       }
     }
-    s2 = wave_sum(s2);
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
-    bn = fmaxf(bn, sqrtf(s2) * 1.0001f);
-    bm = fmaxf(bm, mx);
+    for (int r = 0; r < TS_ROWS; ++r) {
+      const float t2 = wave_sum(s2[r]);
+      float m = mx[r];
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+      bn = fmaxf(bn, sqrtf(t2) * 1.0001f);
+      bm = fmaxf(bm, m);
+    }
   }
   if (lane == 0) { red[0][w] = bn; red[1][w] = bm; }
   __syncthreads();
@@ -340,8 +657,8 @@ __global__ __launch_bounds__(256) void k_table_stats(const float* __restrict__ e
 int launch_table_stats(const float* ent, int64_t E, int Le, float* stats, hipStream_t s) {
   hipError_t e = hipMemsetAsync(stats, 0, 2 * sizeof(float), s);
   if (e != hipSuccess) return (int)e;
-  const int64_t blocks = (E + 3) / 4;  // ≤ 512 blocks: one atomic pair per block
-  hipLaunchKernelGGL(k_table_stats, dim3((unsigned)(blocks < 512 ? blocks : 512)), dim3(256), 0, s, ent, E, Le,
+  const int64_t blocks = (E + 4 * TS_ROWS - 1) / (4 * TS_ROWS);  // ≤ 1024 blocks: one atomic pair per block
+  hipLaunchKernelGGL(k_table_stats, dim3((unsigned)(blocks < 1024 ? blocks : 1024)), dim3(256), 0, s, ent, E, Le,
                      stats);
   return (int)hipGetLastError();
 }

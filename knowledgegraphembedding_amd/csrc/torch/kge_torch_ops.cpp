@@ -295,7 +295,8 @@ std::tuple<Tensor, Tensor> rank_filtered_cuda(const Tensor& entity, const Tensor
                                               int64_t model, double gamma, double erange, int64_t path,
                                               const optional<Tensor>& relation_trig) {
   check_model_mode(model, mode, true);
-  TORCH_CHECK_VALUE(path >= 0 && path <= 3, "rank path ", path, " not supported (0 auto, 1 mfma, 2 tile, 3 scan)");
+  TORCH_CHECK_VALUE(path >= 0 && path <= 4, "rank path ", path,
+                    " not supported (0 auto, 1 mfma, 2 tile, 3 scan, 4 mfma32)");
   const c10::Device dev = require_device({&entity, &relation, modulus ? &*modulus : nullptr, &queries});
   c10::DeviceGuard guard(dev);
   kge_model_desc d = make_desc(model, entity, relation, gamma, erange, modulus);

@@ -384,7 +384,7 @@ def adam_step(param: torch.Tensor, grad: torch.Tensor, exp_avg: torch.Tensor, ex
     )
 
 
-RANK_PATHS = {"auto": 0, "mfma": 1, "tile": 2, "scan": 3}
+RANK_PATHS = {"auto": 0, "mfma": 1, "tile": 2, "scan": 3, "mfma32": 4}
 
 
 def reference_rotation(relation: torch.Tensor, embedding_range: float) -> torch.Tensor:
@@ -411,7 +411,7 @@ def rank_filtered(desc: _lib.ModelDesc, mode: str, queries: torch.Tensor, filt_o
     """Filtered ranks (int64) and tie counts (int32) for a block of queries
     (model.py:383-418), in the reference's fp32 score order
     (kge_rank_filtered_ex).  `path` picks the fast counting pass ("auto",
-    "mfma", "tile", "scan"); `listed` also returns the per-query number of
+    "mfma" = split-bf16 MFMA tile, "mfma32" = fp32 MFMA tile, "tile", "scan"); `listed` also returns the per-query number of
     near-ties that were re-scored; `relation_trig` (RotatE, [R, 2, d] on the
     device, see reference_rotation) is the rotation table the ranks are
     computed with (None: correctly rounded cos / sin)."""

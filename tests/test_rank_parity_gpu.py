@@ -20,8 +20,9 @@ What is asserted, per query (rank = 1 + #{unfiltered e ≠ true: s_e > s_true}):
     rigorous bound δ of what last-bit sin differences can move a gap (below);
     decidable queries must match exactly, the others within the number of
     competitors inside δ, and at most 5 % of the untied queries may differ.
-  * Every fast path (MFMA tile, register tile, wave scan) returns the same
-    ranks and ties bit for bit: their windows differ, the refinement does not.
+  * Every fast path (split-bf16 MFMA tile = "auto" for DistMult / ComplEx,
+    fp32 MFMA tile, register tile, wave scan) returns the same ranks and ties
+    bit for bit: their windows differ, the refinement does not.
   * test_host_trig_matches_reference: this host's torch.cos / torch.sin (what
     KGEModel.test_step uses) against the reference's committed bits; if they
     differ, the reference's RotatE ranks depend on the CPU's vector library,
@@ -44,7 +45,7 @@ pytestmark = pytest.mark.gpu
 DEV = torch.device("cuda", 0)
 U = 2.0 ** -24
 EXACT = ("TransE", "DistMult", "ComplEx", "RotatE")
-PATHS = {"DistMult": ("auto", "tile", "scan"), "ComplEx": ("auto", "tile", "scan"),
+PATHS = {"DistMult": ("auto", "mfma32", "tile", "scan"), "ComplEx": ("auto", "mfma32", "tile", "scan"),
          "TransE": ("auto", "scan"), "RotatE": ("auto", "scan"), "pRotatE": ("auto", "scan")}
 
 
@@ -212,3 +213,34 @@ def test_host_trig_matches_reference(g_full, golden_info, capsys):
         with capsys.disabled():
             print(f"  {mode}: ranks from this host's cos/sin differ from the reference's on "
                   f"{int((ranks != r_rank).sum())} of {nq} queries")
+
+
+@pytest.mark.parametrize("name,E,d", [("DistMult", 300, 50), ("DistMult", 257, 37), ("DistMult", 1000, 130),
+                                      ("ComplEx", 300, 25), ("ComplEx", 513, 33), ("DistMult", 129, 16)])
+def test_split_bf16_tile_matches_other_paths(name, E, d):
+    """The split-bf16 MFMA tile ("auto" for DistMult / ComplEx) against the
+    fp32 paths on shapes its layout pads: E not a multiple of the 128-row
+    block, reduction lengths not a multiple of the 16-k slab (and odd ones,
+    whose rows are not float4-aligned), plus exact ties — a block of entity
+    rows copied from a true entity.  Ranks and tie counts must be identical
+    to the wave scan's (reference order after refinement on every path)."""
+    R = 7
+    m, ent, rel, _, _ = build(name, E, R, d, 12.0, 17)
+    with torch.no_grad():
+        m.entity_embedding[E - 9:E - 1].copy_(m.entity_embedding[3].expand(8, -1))  # 8 exact copies of entity 3
+    g = np.random.default_rng(5)
+    q = np.stack([g.integers(0, E, 200), g.integers(0, R, 200), g.integers(0, E, 200)], 1).astype(np.int64)
+    q[:20, 0] = 3
+    q[20:40, 2] = 3
+    true = np.unique(np.concatenate([q, np.stack([g.integers(0, E, 600), g.integers(0, R, 600),
+                                                  g.integers(0, E, 600)], 1)]), axis=0)
+    le = 2 * d if name == "ComplEx" else d
+    paths = ["scan", "auto"] + (["mfma32"] if le % 4 == 0 else [])
+    for mode in ("head-batch", "tail-batch"):
+        out = {p: m.rank_queries(q, true, mode, path=p, listed=True) for p in paths}
+        r0, t0, _ = out["scan"]
+        tied = slice(0, 20) if mode == "head-batch" else slice(20, 40)  # true entity 3, copied 8 times
+        assert (t0[tied] > 0).any(), (name, mode)
+        for p in paths[1:]:
+            r, t, _ = out[p]
+            assert np.array_equal(r, r0) and np.array_equal(t, t0), (name, E, d, mode, p)

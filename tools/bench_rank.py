@@ -35,7 +35,9 @@ def rank_path(name, K, path="auto"):
     """Which fast pass kge_rank_filtered_ex runs (kge_capi.hip rank_path)."""
     red = K // 2 if name in ("RotatE", "ComplEx") else K
     mfma_ok = name in ("DistMult", "ComplEx") and K % 4 == 0
-    if path == "mfma" or (path == "auto" and mfma_ok):
+    if path == "mfma" or (path == "auto" and name in ("DistMult", "ComplEx")):
+        return "mfma-split-bf16"
+    if path == "mfma32" or (path == "auto" and mfma_ok):
         return "mfma"
     if path in ("auto", "tile") and red % 4 == 0:
         return "valu-tile"
@@ -47,7 +49,7 @@ def main():
     ap.add_argument("--models", nargs="+", default=["DistMult", "ComplEx"])
     ap.add_argument("-d", "--hidden_dim", type=int, default=500)
     ap.add_argument("--reps", type=int, default=3)
-    ap.add_argument("--path", default="auto", choices=("auto", "mfma", "tile", "scan"))
+    ap.add_argument("--path", default="auto", choices=("auto", "mfma", "mfma32", "tile", "scan"))
     ap.add_argument("--cpu-sample", type=int, default=0, help="queries timed through the CPU oracle (0: skip)")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
@@ -83,7 +85,7 @@ def main():
                "path": rank_path(name, K, a.path),
                "pair_terms_per_s": nq * E * (K // 2 if name in ("RotatE", "ComplEx") else K) / dt,
                "mrr": float(np.mean(1.0 / ranks))}
-        if res["path"] == "mfma":
+        if res["path"].startswith("mfma"):
             res["roofline"] = {"bound": "mfma", "achieved": res["tflops"], "peak": FP32_PEAK_TF, "unit": "TFLOP/s",
                                "frac": res["tflops"] / FP32_PEAK_TF}
         if a.cpu_sample:
