@@ -882,7 +882,7 @@ RankWs carve_rank(void* ws, const kge_model_desc* m, int64_t nq, size_t* bytes) 
   w.s_true = c.take<float>(nq);
   w.sref_true = c.take<float>(nq);
   w.delta = c.take<float>(nq);
-  w.stats = c.take<float>(4);
+  w.stats = c.take<float>(2 + 2 * TS_BLOCKS);  // [max ‖e‖, max |x|, per-block partials]
   w.true_id = c.take<int64_t>(nq);
   w.gt = c.take<int32_t>(5 * nq);  // gt, eq, gtx, eqx, ucnt: one memset
   w.eq = w.gt ? w.gt + nq : nullptr;
@@ -929,8 +929,7 @@ int kge_rank_filtered_ex(const kge_model_desc* m, int32_t mode, const int64_t* q
   RankWs w = carve_rank(workspace, m, nq, &need);
   if (!workspace || workspace_bytes < need) return KGE_ERR_WORKSPACE;
   hipStream_t s = as_stream(stream);
-  hipError_t e = hipMemsetAsync(w.gt, 0, sizeof(int32_t) * 5 * nq, s);
-  if (e != hipSuccess) return hip_status(e);
+  // (gt, eq, gtx, eqx, ucnt are zeroed by k_rank_prep: RankArgs.zero_counts)
   const ModelOps& ops = ops_for(m->model);
   const bool cplx = (m->model == KGE_ROTATE || m->model == KGE_COMPLEX);
   const int K = cplx ? m->entity_dim / 2 : m->entity_dim;
@@ -948,6 +947,7 @@ int kge_rank_filtered_ex(const kge_model_desc* m, int32_t mode, const int64_t* q
   a.q = w.q; a.s_true = w.s_true; a.true_id = w.true_id; a.gt = w.gt;
   a.fbits = w.bits; a.W = (m->nentity + 31) / 32; a.win = win; a.err = err_flag;
   a.prep_only = 1;
+  a.zero_counts = 1;
   a.trig = trig;
   st = launch_status(ops.rank(mode, geo.vec, geo.ns, a, s));
   if (st) return st;
@@ -1003,6 +1003,7 @@ int kge_rank_filtered_ex(const kge_model_desc* m, int32_t mode, const int64_t* q
     st = launch_status(ops.rank_tile(mode, 0, ta, s));
   } else {
     a.prep_only = 0;
+    a.zero_counts = 0;
     st = launch_status(ops.rank(mode, geo.vec, geo.ns, a, s));
   }
   if (st) return st;

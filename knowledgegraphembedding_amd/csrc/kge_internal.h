@@ -168,6 +168,7 @@ struct RankArgs {
   RankWin win;
   int32_t* err;
   int prep_only;        // launch k_rank_prep only (the MFMA / tile paths count on their own)
+  int zero_counts;      // k_rank_prep zeroes gt and the four [nq] counters after it (eq, gtx, eqx, ucnt)
   const float* trig;    // RotatE: [R, 2, Lr] reference cos | sin of the phases, or null
 };
 

@@ -21,6 +21,7 @@
 // exact and order-free.  Candidates within the query's near-tie window are not
 // counted but listed (win_count) for the reference-order refinement
 // (kge_rank_ref.h): the fma order here is not the reference's sum order.
+#include <algorithm>
 #include <cstdlib>
 
 #include "kge_common.h"
@@ -347,6 +348,7 @@ struct XArgs {
   uint32_t qs_bytes, es_bytes;
   int64_t nq, E;
   int nslab;
+  int gx, gy, group;   // counting pass: candidate / query tiles, candidate tiles per L2 group (xcd_tile)
   const int64_t* true_id;
   float* s_true;
   const uint32_t* fbits;
@@ -354,6 +356,26 @@ struct XArgs {
   int32_t* gt;
   RankWin win;
 };
+
+// Counting pass tile order.  Workgroups are dealt to the 8 XCDs round-robin
+// (b mod 8), each XCD with its own 4 MB L2.  XCD k takes the candidate tiles
+// x ≡ k (mod 8) in groups of `group` tiles (≤ 2 MB of split rows) and runs
+// every query tile against one group before the next: a candidate tile is
+// fetched into that L2 once per group instead of once per query tile (the
+// plain grid re-read the whole 84 MB split table from MALL for each of
+// wn18rr's 25 query tiles: 2.2 GB per launch, 43 % MFMA-busy).  The order is
+// a speed property only.  Returns false for the grid's idle tail blocks.
+__device__ __forceinline__ bool xcd_tile(const XArgs& a, int& x, int& y) {
+  const int b = blockIdx.x, k = b & 7, i = b >> 3;
+  const int nxk = (a.gx - k + 7) >> 3;  // candidate tiles of XCD k
+  if (i >= nxk * a.gy) return false;
+  const int per = a.group * a.gy;
+  const int g = i / per, rem = i - g * per;
+  const int gsz = min(a.group, nxk - g * a.group);
+  x = (g * a.group + rem % gsz) * 8 + k;
+  y = rem / gsz;
+  return true;
+}
 
 template <bool GATHER>
 __global__ __launch_bounds__(256, 2) void k_rank_mfma_x(XArgs a) {
@@ -366,8 +388,10 @@ __global__ __launch_bounds__(256, 2) void k_rank_mfma_x(XArgs a) {
   int32_t* cgt = reinterpret_cast<int32_t*>(sdl + 128);
   const int t = threadIdx.x, lane = t & 63, w = wave_id();
   const int wm = w >> 1, wn = w & 1;
-  const int64_t q0 = (int64_t)blockIdx.y * BM;
-  const int64_t e0 = (int64_t)blockIdx.x * BN;
+  int tx = 0, ty = (int)blockIdx.y;
+  if (!GATHER && !xcd_tile(a, tx, ty)) return;  // (block-uniform)
+  const int64_t q0 = (int64_t)ty * BM;
+  const int64_t e0 = (int64_t)tx * BN;
   if (t < 128) {
     const int64_t q = q0 + t;
     arow[t] = (q < a.nq) ? q : -1;
@@ -391,7 +415,7 @@ __global__ __launch_bounds__(256, 2) void k_rank_mfma_x(XArgs a) {
   int64_t grow[4];  // GATHER, E pieces: this lane's source row of chunk c (row c·32 + lane/2)
 #pragma unroll
   for (int c = 0; c < 4; ++c) grow[c] = (GATHER && !wq) ? brow[c * 32 + (lane >> 1)] : 0;
-  const int64_t rb_tile = wq ? (int64_t)blockIdx.y : (int64_t)blockIdx.x;
+  const int64_t rb_tile = wq ? (int64_t)ty : (int64_t)tx;
   auto issue = [&](int sl, int st) {
     uint16_t* base = smem + (st * 4 + w) * XS_PIECE;
 #pragma unroll
@@ -587,24 +611,29 @@ int launch_rank_mfma_x(int gather, const uint16_t* qs, const uint16_t* es, int64
   a.qs_bytes = (uint32_t)qb; a.es_bytes = (uint32_t)eb;
   a.true_id = true_id; a.s_true = s_true; a.fbits = bits; a.W = (E + 31) / 32; a.gt = gt; a.win = win;
   const unsigned gy = (unsigned)((nq + BM - 1) / BM);
+  a.gx = (int)((E + BN - 1) / BN);
+  a.gy = (int)gy;
+  // candidate tiles per L2 group: ≤ 2 MB of split rows (half an XCD's L2)
+  const int64_t tile_bytes = (int64_t)BN * a.nslab * XS_BK * 4;
+  a.group = (int)std::max<int64_t>(1, (2 << 20) / tile_bytes);
   // __launch_bounds__(256, 2): 64 KB ring + 4.4 KB, ≤ 256 VGPRs — 2 workgroups = 2 waves per SIMD
   if (gather) {
     hipLaunchKernelGGL((k_rank_mfma_x<true>), dim3(1, gy), dim3(256), 0, s, a);
   } else {
-    const dim3 gs((unsigned)((E + BN - 1) / BN), gy);
-    hipLaunchKernelGGL((k_rank_mfma_x<false>), gs, dim3(256), 0, s, a);
+    const int64_t per_xcd = (int64_t)((a.gx + 7) / 8) * a.gy;  // XCD 0 has the most candidate tiles
+    hipLaunchKernelGGL((k_rank_mfma_x<false>), dim3((unsigned)(8 * per_xcd)), dim3(256), 0, s, a);
   }
   return (int)hipGetLastError();
 }
 
 // Entity-table statistics for the ranking windows: stats[0] = max row L2
-// norm, stats[1] = max |x| (non-negative floats order like their bit
-// patterns, so an integer atomicMax is exact).  Each wave takes TS_ROWS rows
-// at a time with their loads interleaved (TS_ROWS float4s in flight per lane;
-// one row per wave at a time left the pass latency-bound: 0.24 ms for
-// wn18rr's 40,943 × 500 table, r02), rows strided over a bounded grid; the
-// block's four waves combine in LDS and the block issues one atomic per
-// statistic (an atomic per row on the same two words serialised: 0.93 ms).
+// norm, stats[1] = max |x|.  Each wave takes TS_ROWS rows at a time with their
+// loads interleaved (TS_ROWS float4s in flight per lane; one row per wave at a
+// time left the pass latency-bound: 0.24 ms for wn18rr's 40,943 × 500 table,
+// r02), rows strided over a bounded grid; each block writes its two partial
+// maxima to stats[2 + 2·block] and one small block reduces them (the
+// per-block atomics on the same two words serialised at ≈11 ns each: 23 µs of
+// the 35 µs pass; per row, 0.93 ms).  stats needs 2 + 2·TS_BLOCKS floats.
 constexpr int TS_ROWS = 4;
 __global__ __launch_bounds__(256) void k_table_stats(const float* __restrict__ ent, int64_t E, int Le,
                                                      float* stats) {
@@ -647,19 +676,39 @@ __global__ __launch_bounds__(256) void k_table_stats(const float* __restrict__ e
   if (lane == 0) { red[0][w] = bn; red[1][w] = bm; }
   __syncthreads();
   if (threadIdx.x == 0) {
-    const float n = fmaxf(fmaxf(red[0][0], red[0][1]), fmaxf(red[0][2], red[0][3]));
-    const float m = fmaxf(fmaxf(red[1][0], red[1][1]), fmaxf(red[1][2], red[1][3]));
-    atomicMax(reinterpret_cast<unsigned int*>(&stats[0]), __float_as_uint(n));
-    atomicMax(reinterpret_cast<unsigned int*>(&stats[1]), __float_as_uint(m));
+    stats[2 + 2 * blockIdx.x] = fmaxf(fmaxf(red[0][0], red[0][1]), fmaxf(red[0][2], red[0][3]));
+    stats[3 + 2 * blockIdx.x] = fmaxf(fmaxf(red[1][0], red[1][1]), fmaxf(red[1][2], red[1][3]));
+  }
+}
+
+__global__ __launch_bounds__(256) void k_stats_reduce(float* stats, int nblocks) {
+  __shared__ float red[2][4];
+  const int lane = threadIdx.x & 63, w = wave_id();
+  float n = 0.f, m = 0.f;
+  for (int b = threadIdx.x; b < nblocks; b += 256) {
+    n = fmaxf(n, stats[2 + 2 * b]);
+    m = fmaxf(m, stats[3 + 2 * b]);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    n = fmaxf(n, __shfl_xor(n, o));
+    m = fmaxf(m, __shfl_xor(m, o));
+  }
+  if (lane == 0) { red[0][w] = n; red[1][w] = m; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    stats[0] = fmaxf(fmaxf(red[0][0], red[0][1]), fmaxf(red[0][2], red[0][3]));
+    stats[1] = fmaxf(fmaxf(red[1][0], red[1][1]), fmaxf(red[1][2], red[1][3]));
   }
 }
 
 int launch_table_stats(const float* ent, int64_t E, int Le, float* stats, hipStream_t s) {
-  hipError_t e = hipMemsetAsync(stats, 0, 2 * sizeof(float), s);
+  const int64_t want = (E + 4 * TS_ROWS - 1) / (4 * TS_ROWS);
+  const int blocks = (int)(want < TS_BLOCKS ? (want > 0 ? want : 1) : TS_BLOCKS);
+  hipLaunchKernelGGL(k_table_stats, dim3((unsigned)blocks), dim3(256), 0, s, ent, E, Le, stats);
+  hipError_t e = hipGetLastError();
   if (e != hipSuccess) return (int)e;
-  const int64_t blocks = (E + 4 * TS_ROWS - 1) / (4 * TS_ROWS);  // ≤ 1024 blocks: one atomic pair per block
-  hipLaunchKernelGGL(k_table_stats, dim3((unsigned)(blocks < 1024 ? blocks : 1024)), dim3(256), 0, s, ent, E, Le,
-                     stats);
+  hipLaunchKernelGGL(k_stats_reduce, dim3(1), dim3(256), 0, s, stats, blocks);
   return (int)hipGetLastError();
 }
 

@@ -553,16 +553,36 @@ class KGEModel(nn.Module):
         index = all_true_triples if isinstance(all_true_triples, FilterIndex) else \
             FilterIndex(all_true_triples, self.nentity, self.nrelation)
         q = np.asarray(triples, dtype=np.int64).reshape(-1, 3)
+        nq = len(q)
         outs = []
         with torch.no_grad():
             trig = self._rank_rotation(dev, relation_trig)
+            qd = None
             for mode in ('head-batch', 'tail-batch'):
+                # the direction's inputs in one pinned host buffer, copied
+                # asynchronously: the tail's filter CSR is built on the host
+                # while the head direction's kernels run, and its copy queues
+                # behind them without blocking the host
                 off, ids = index.filter_csr(q, mode)
-                outs.append(ops.rank_filtered(self.desc(), mode, torch.from_numpy(q), torch.from_numpy(off),
-                                              torch.from_numpy(ids), dev, path=path, relation_trig=trig))
-        res = tuple(tuple(t.cpu().numpy() for t in out) for out in outs)
-        ops.raise_on_device_error(dev)
-        return res
+                parts = ([q.reshape(-1)] if qd is None else []) + [off, ids if len(ids) else np.zeros(1, np.int64)]
+                flat = torch.from_numpy(np.concatenate(parts).astype(np.int64, copy=False)).pin_memory()
+                flat = flat.to(dev, non_blocking=True)
+                if qd is None:
+                    qd, flat = flat[:3 * nq].view(nq, 3), flat[3 * nq:]
+                outs.append(ops.rank_filtered(self.desc(), mode, qd, flat[:nq + 1], flat[nq + 1:], dev, path=path,
+                                              relation_trig=trig))
+            # one device → host copy (pinned): both directions' ranks (int64 as
+            # int32 pairs) and ties, and the error flag
+            packed = torch.cat([outs[0][0].view(torch.int32), outs[1][0].view(torch.int32), outs[0][1], outs[1][1],
+                                ops.state(dev).err])
+            host = torch.empty(packed.shape, dtype=torch.int32, pin_memory=True)
+            host.copy_(packed, non_blocking=True)
+            torch.cuda.current_stream(dev).synchronize()
+        h = host.numpy()
+        ops.raise_device_error_value(dev, int(h[-1]))
+        rh, rt = h[:2 * nq].view(np.int64).copy(), h[2 * nq:4 * nq].view(np.int64).copy()
+        th, tt = h[4 * nq:5 * nq].copy(), h[5 * nq:6 * nq].copy()
+        return (rh, th), (rt, tt)
 
     def rank_queries(self, triples, all_true_triples, mode, path="auto", listed=False, relation_trig=None):
         """Per-query filtered ranks and tie counts (numpy int64, int32) — the

@@ -81,8 +81,12 @@ def state(dev: torch.device) -> _DeviceState:
 
 def raise_on_device_error(dev: torch.device) -> None:
     """Read (and clear) the device error flag — a sync point."""
+    raise_device_error_value(dev, int(state(dev).err.item()))
+
+
+def raise_device_error_value(dev: torch.device, v: int) -> None:
+    """Raise for an error-flag value already read back (and clear the flag)."""
     st = state(dev)
-    v = int(st.err.item())
     if v:
         st.err.zero_()
         if v & _lib.DEVERR_INDEX:
