@@ -292,6 +292,7 @@ __global__ __launch_bounds__(256) void k_rank_emit(EmitArgs a) {
 // zeros in the split buffers.  256 threads as 2×2 waves of 64×64 (2×2 MFMA
 // tiles), 4-stage LDS ring (64 KB) with 3 slabs in flight, 2 workgroups per CU.
 typedef short bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 constexpr int XS_BK = 16;                   // k per slab = one 32x32x16 MFMA step
 constexpr int XS_PIECE = 128 * XS_BK;       // bf16 per (row block, slab, hi|lo) = 4 KB
 constexpr int XS_NST = 4;                   // LDS ring stages
@@ -377,7 +378,9 @@ __device__ __forceinline__ bool xcd_tile(const XArgs& a, int& x, int& y) {
   return true;
 }
 
-template <bool GATHER>
+// DIAG (timing diagnostics only, wrong ranks; KGE_XTILE_DIAG): 1 = no MFMAs,
+// 2 = no LDS-DMA (MFMAs on whatever the ring holds)
+template <bool GATHER, int DIAG = 0>
 __global__ __launch_bounds__(256, 2) void k_rank_mfma_x(XArgs a) {
   // one LDS array: [XS_NST stages][E_hi | E_lo | Q_hi | Q_lo] then arow/brow, sts, sdl, cgt
   __shared__ __attribute__((aligned(16))) uint16_t smem[XS_NST * 4 * XS_PIECE + 128 * 4 * 2 + 128 * 2 * 2 + 128 * 2 * 3];
@@ -417,6 +420,7 @@ __global__ __launch_bounds__(256, 2) void k_rank_mfma_x(XArgs a) {
   for (int c = 0; c < 4; ++c) grow[c] = (GATHER && !wq) ? brow[c * 32 + (lane >> 1)] : 0;
   const int64_t rb_tile = wq ? (int64_t)ty : (int64_t)tx;
   auto issue = [&](int sl, int st) {
+    if (DIAG == 2) return;
     uint16_t* base = smem + (st * 4 + w) * XS_PIECE;
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
@@ -443,13 +447,13 @@ __global__ __launch_bounds__(256, 2) void k_rank_mfma_x(XArgs a) {
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   };
 
-  f32x16 run[2][2], cor[2][2];
+  f32x16 run[2][2], cor[2][2], mprev[2][2];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) run[i][j][r] = cor[i][j][r] = 0.f;
+      for (int r = 0; r < 16; ++r) run[i][j][r] = cor[i][j][r] = mprev[i][j][r] = 0.f;
   const f32x16 zero = {};
 
   const int kh = lane >> 5, li = lane & 31;
@@ -462,7 +466,7 @@ __global__ __launch_bounds__(256, 2) void k_rank_mfma_x(XArgs a) {
     __builtin_amdgcn_s_barrier();  // ... every wave's; slab sl-1's reads are done (no fence: the
                                    // vmcnt above covers the DMA, __syncthreads' would be vmcnt(0))
     if (sl + XS_NST - 1 < nslab) issue(sl + XS_NST - 1, (sl + XS_NST - 1) % XS_NST);
-    if (!live) continue;
+    if (!live || DIAG == 1) continue;
     const uint16_t* Eh = smem + (sl % XS_NST) * 4 * XS_PIECE;
     const uint16_t* El = Eh + XS_PIECE;
     const uint16_t* Qh = Eh + 2 * XS_PIECE;
@@ -480,12 +484,22 @@ __global__ __launch_bounds__(256, 2) void k_rank_mfma_x(XArgs a) {
       qh[j] = *reinterpret_cast<const bf16x8*>(Qh + row * XS_BK + kh * 8);
       ql[j] = *reinterpret_cast<const bf16x8*>(Ql + row * XS_BK + kh * 8);
     }
+    // the running sum takes the PREVIOUS slab's hi·hi products (long done:
+    // an add right behind the MFMA it reads stalls the wave ~40 cycles), then
+    // this slab's four hi·hi and twelve correction MFMAs
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
-        const f32x16 m = __builtin_amdgcn_mfma_f32_32x32x16_bf16(eh[i], qh[j], zero, 0, 0, 0);
-        run[i][j] += m;
+#pragma unroll
+        for (int r = 0; r < 16; r += 2) {
+          f32x2 x = {run[i][j][r], run[i][j][r + 1]};
+          const f32x2 y = {mprev[i][j][r], mprev[i][j][r + 1]};
+          x += y;
+          run[i][j][r] = x.x;
+          run[i][j][r + 1] = x.y;
+        }
+        mprev[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(eh[i], qh[j], zero, 0, 0, 0);
         cor[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(eh[i], ql[j], cor[i][j], 0, 0, 0);
         cor[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(el[i], qh[j], cor[i][j], 0, 0, 0);
         cor[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(el[i], ql[j], cor[i][j], 0, 0, 0);
@@ -495,7 +509,7 @@ __global__ __launch_bounds__(256, 2) void k_rank_mfma_x(XArgs a) {
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = run[i][j] + cor[i][j];
+    for (int j = 0; j < 2; ++j) acc[i][j] = (run[i][j] + mprev[i][j]) + cor[i][j];
 
   // C/D layout as the fp32 tile: col (query) = lane & 31, row (candidate) = (reg & 3) + 8·(reg >> 2) + 4·(lane >> 5)
   if (GATHER) {
@@ -621,7 +635,16 @@ int launch_rank_mfma_x(int gather, const uint16_t* qs, const uint16_t* es, int64
     hipLaunchKernelGGL((k_rank_mfma_x<true>), dim3(1, gy), dim3(256), 0, s, a);
   } else {
     const int64_t per_xcd = (int64_t)((a.gx + 7) / 8) * a.gy;  // XCD 0 has the most candidate tiles
-    hipLaunchKernelGGL((k_rank_mfma_x<false>), dim3((unsigned)(8 * per_xcd)), dim3(256), 0, s, a);
+    const char* dg = getenv("KGE_XTILE_DIAG");  // timing diagnostics (tools/ab_rank)
+    const int diag = dg ? atoi(dg) : 0;
+    if (const char* gg = getenv("KGE_XTILE_GROUP")) a.group = std::max(1, atoi(gg));
+    const dim3 gs((unsigned)(8 * per_xcd));
+    if (diag == 1)
+      hipLaunchKernelGGL((k_rank_mfma_x<false, 1>), gs, dim3(256), 0, s, a);
+    else if (diag == 2)
+      hipLaunchKernelGGL((k_rank_mfma_x<false, 2>), gs, dim3(256), 0, s, a);
+    else
+      hipLaunchKernelGGL((k_rank_mfma_x<false>), gs, dim3(256), 0, s, a);
   }
   return (int)hipGetLastError();
 }
