@@ -140,6 +140,22 @@ __global__ __launch_bounds__(256, 4) void k_rank_mfma(MfmaArgs a) {
   // goes to the co-resident workgroups (wn = 1 of the last query row of
   // blocks for wn18rr's 3134 queries: 2 % of the launch)
   const bool live = q0 + wn * 64 < a.nq && (GATHER || e0 + wm * 64 < a.E);
+  // the epilogue's exclusion-bitmap words, loaded now so their latency hides
+  // behind the K loop (loaded at the end they cost two memory round trips
+  // per block: with the split tile 19 % of the launch)
+  uint32_t exw[2][2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int64_t q = q0 + wn * 64 + j * 32 + (lane & 31);
+      const int64_t widx = (e0 >> 5) + wm * 2 + i;
+      const int64_t cbase = e0 + wm * 64 + i * 32;
+      uint32_t word = (!GATHER && q < a.nq && widx < a.W) ? a.fbits[q * a.W + widx] : ~0u;
+      const int64_t valid = a.E - cbase;
+      if (valid < 32) word |= (valid <= 0) ? ~0u : (~0u << valid);
+      exw[j][i] = word;
+    }
   issue(0, 0);
   for (int s = 0; s < nslab; ++s) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA of slab s has landed
@@ -191,37 +207,37 @@ __global__ __launch_bounds__(256, 4) void k_rank_mfma(MfmaArgs a) {
     }
     return;
   }
-  const int64_t wbase = e0 >> 5;
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     const int n = wn * 64 + j * 32 + li;
     const int64_t q = arow[n];
     const float st = sts[n], dlt = sdl[n];
-    uint32_t ex[2];
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int64_t widx = wbase + wm * 2 + i;
-      const int64_t cbase = e0 + wm * 64 + i * 32;
-      uint32_t word = (q >= 0 && widx < a.W) ? a.fbits[q * a.W + widx] : ~0u;
-      const int64_t valid = a.E - cbase;
-      if (valid < 32) word |= (valid <= 0) ? ~0u : (~0u << valid);
-      ex[i] = word;
-    }
+    const uint32_t ex[2] = {exw[j][0], exw[j][1]};
+    // branch-free count; the rare near-ties collect in a bit mask and are
+    // listed in one loop afterwards (a branch per candidate cost more than
+    // the count itself)
     int g = 0;
+    uint32_t near = 0;  // bit 16·i + r
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int mloc = (r & 3) + 8 * (r >> 2) + 4 * kh;
         const bool ok = ((ex[i] >> mloc) & 1u) == 0u;
-        const float sc = acc[i][j][r];
-        const float diff = sc - st;
+        const float diff = acc[i][j][r] - st;
         g += (ok && diff > dlt) ? 1 : 0;
-        if (ok && !(diff > dlt) && diff >= -dlt) {
-          const int idx = atomicAdd(&a.win.ucnt[q], 1);
-          if (idx < a.win.cap) a.win.ulist[q * (int64_t)a.win.cap + idx] = (int32_t)(e0 + wm * 64 + i * 32 + mloc);
-        }
+        near |= (ok && !(diff > dlt) && diff >= -dlt) ? (1u << (16 * i + r)) : 0u;
       }
+    if (__builtin_amdgcn_ballot_w64(near != 0u)) {
+      while (near) {
+        const int b = __builtin_ctz(near);
+        near &= near - 1u;
+        const int i = b >> 4, r = b & 15;
+        const int mloc = (r & 3) + 8 * (r >> 2) + 4 * kh;
+        const int idx = atomicAdd(&a.win.ucnt[q], 1);
+        if (idx < a.win.cap) a.win.ulist[q * (int64_t)a.win.cap + idx] = (int32_t)(e0 + wm * 64 + i * 32 + mloc);
+      }
+    }
     g += __shfl_xor(g, 32);
     if (kh == 0 && q >= 0 && g) atomicAdd(&cgt[n], g);
   }
@@ -378,13 +394,27 @@ __device__ __forceinline__ bool xcd_tile(const XArgs& a, int& x, int& y) {
   return true;
 }
 
+// TQ = query column tiles (32 each) per wave: a workgroup is 2 × 2 waves
+// over 128 candidates × 64·TQ queries.  TQ = 2 (default): 64×64 per wave,
+// 239 VGPRs, 64 KB ring, 2 workgroups per CU.  TQ = 1 (KGE_XTILE_TQ=1): 64×32
+// per wave, 133 VGPRs, a 48 KB ring, 3 workgroups per CU — more waves per SIMD
+// for 1.5× the fragment reads per MFMA and twice the candidate-tile DMAs;
+// measured equal (530 vs 523 µs, profiles/r03/rank/ab_tile_variants.txt).
 // DIAG (timing diagnostics only, wrong ranks; KGE_XTILE_DIAG): 1 = no MFMAs,
-// 2 = no LDS-DMA (MFMAs on whatever the ring holds)
-template <bool GATHER, int DIAG = 0>
-__global__ __launch_bounds__(256, 2) void k_rank_mfma_x(XArgs a) {
+// 2 = no LDS-DMA (MFMAs on whatever the ring holds), 3 = no epilogue.
+template <int TQ>
+struct XTile {
+  static constexpr int BQ = 64 * TQ;                   // queries per workgroup
+  static constexpr int STAGE = (8 + 4 * TQ) * 512;     // bf16 per ring stage: E hi|lo (4 KB each), Q hi|lo (2·TQ KB each)
+  static constexpr int CPW = 2 + TQ;                   // 1 KB DMA chunks per wave per slab
+};
+
+template <bool GATHER, int TQ, int DIAG = 0>
+__global__ __launch_bounds__(256, TQ == 1 ? 3 : 2) void k_rank_mfma_x(XArgs a) {
+  using X = XTile<TQ>;
   // one LDS array: [XS_NST stages][E_hi | E_lo | Q_hi | Q_lo] then arow/brow, sts, sdl, cgt
-  __shared__ __attribute__((aligned(16))) uint16_t smem[XS_NST * 4 * XS_PIECE + 128 * 4 * 2 + 128 * 2 * 2 + 128 * 2 * 3];
-  int64_t* arow = reinterpret_cast<int64_t*>(smem + XS_NST * 4 * XS_PIECE);
+  __shared__ __attribute__((aligned(16))) uint16_t smem[XS_NST * X::STAGE + 128 * 4 * 2 + 128 * 2 * 2 + 128 * 2 * 3];
+  int64_t* arow = reinterpret_cast<int64_t*>(smem + XS_NST * X::STAGE);
   int64_t* brow = arow + 128;
   float* sts = reinterpret_cast<float*>(brow + 128);
   float* sdl = sts + 128;
@@ -393,17 +423,18 @@ __global__ __launch_bounds__(256, 2) void k_rank_mfma_x(XArgs a) {
   const int wm = w >> 1, wn = w & 1;
   int tx = 0, ty = (int)blockIdx.y;
   if (!GATHER && !xcd_tile(a, tx, ty)) return;  // (block-uniform)
-  const int64_t q0 = (int64_t)ty * BM;
+  const int64_t q0 = (int64_t)ty * X::BQ;
   const int64_t e0 = (int64_t)tx * BN;
   if (t < 128) {
     const int64_t q = q0 + t;
-    arow[t] = (q < a.nq) ? q : -1;
-    const int64_t tid_ = (q < a.nq) ? a.true_id[q] : -1;
+    const bool in = t < X::BQ && q < a.nq;
+    arow[t] = in ? q : -1;
+    const int64_t tid_ = in ? a.true_id[q] : -1;
     if (GATHER) {
-      brow[t] = (tid_ >= 0 && tid_ < a.E) ? tid_ : -1;
+      brow[t] = (tid_ >= 0 && tid_ < a.E) ? tid_ : -1;  // candidate row t = query t's true entity
     } else {
-      sts[t] = (q < a.nq) ? a.s_true[q] : 0.f;
-      sdl[t] = (q < a.nq) ? a.win.delta[q] : 0.f;
+      sts[t] = in ? a.s_true[q] : 0.f;
+      sdl[t] = in ? a.win.delta[q] : 0.f;
     }
     cgt[t] = 0;
   }
@@ -412,66 +443,100 @@ __global__ __launch_bounds__(256, 2) void k_rank_mfma_x(XArgs a) {
   const auto rq = buf_rsrc(a.qs, a.qs_bytes);
   const auto re = buf_rsrc(a.es, a.es_bytes);
   const int nslab = a.nslab;
-  // wave w moves piece w of every slab: 0 E_hi, 1 E_lo, 2 Q_hi, 3 Q_lo (4 × 1 KB)
-  const bool wq = w >= 2;
-  const int piece = w & 1;
-  int64_t grow[4];  // GATHER, E pieces: this lane's source row of chunk c (row c·32 + lane/2)
+  // 1 KB chunk c of a stage (LDS bytes c·1024 …): c < 8 candidate pieces
+  // (hi: 0-3, lo: 4-7; 32 rows each), then the query pieces (hi, lo: 2·TQ
+  // chunks each).  Wave w moves chunks CPW·w … CPW·w + CPW − 1.
+  int64_t grow[X::CPW];  // GATHER: this lane's source row of each candidate chunk
 #pragma unroll
-  for (int c = 0; c < 4; ++c) grow[c] = (GATHER && !wq) ? brow[c * 32 + (lane >> 1)] : 0;
-  const int64_t rb_tile = wq ? (int64_t)ty : (int64_t)tx;
+  for (int k = 0; k < X::CPW; ++k) {
+    const int c = X::CPW * w + k;
+    grow[k] = (GATHER && c < 8) ? brow[(c & 3) * 32 + (lane >> 1)] : 0;
+  }
+  const int64_t qrb = (int64_t)ty * X::BQ / 128;           // the queries' 128-row block in the split layout
+  const uint32_t qsub = (uint32_t)((ty * X::BQ) & 127) * 32;  // … and their byte offset inside it
   auto issue = [&](int sl, int st) {
     if (DIAG == 2) return;
-    uint16_t* base = smem + (st * 4 + w) * XS_PIECE;
+    uint16_t* base = smem + st * X::STAGE;
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
+    for (int k = 0; k < X::CPW; ++k) {
+      const int c = X::CPW * w + k;
       uint32_t off;
-      if (GATHER && !wq) {
-        const int64_t r = grow[c];
-        off = (r >= 0) ? (uint32_t)((((r >> 7) * nslab + sl) * 2 + piece) * (2 * XS_PIECE) + (r & 127) * 32 +
-                                    (lane & 1) * 16)
-                       : XS_OOB;
+      const bool cand = c < 8;
+      if (cand) {
+        const int piece = c >> 2, sub = c & 3;
+        if (GATHER) {
+          const int64_t r = grow[k];
+          off = (r >= 0) ? (uint32_t)((((r >> 7) * nslab + sl) * 2 + piece) * (2 * XS_PIECE) + (r & 127) * 32 +
+                                      (lane & 1) * 16)
+                         : XS_OOB;
+        } else {
+          off = (uint32_t)((((int64_t)tx * nslab + sl) * 2 + piece) * (2 * XS_PIECE) + sub * 1024 + lane * 16);
+        }
       } else {
-        off = (uint32_t)(((rb_tile * nslab + sl) * 2 + piece) * (2 * XS_PIECE) + c * 1024 + lane * 16);
+        const int cc = c - 8, piece = cc / (2 * TQ), sub = cc % (2 * TQ);
+        off = (uint32_t)(((qrb * nslab + sl) * 2 + piece) * (2 * XS_PIECE) + qsub + sub * 1024 + lane * 16);
       }
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(wq ? rq : re,
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(cand ? re : rq,
                                                (__attribute__((address_space(3))) void*)(base + c * 512), 16, off,
                                                0, 0, 0);
     }
   };
   // DMAs issued after slab sl's, when sl is waited for: those of the next
-  // min(2, nslab − 1 − sl) slabs, 4 instructions each (vmcnt counts in order)
+  // min(XS_NST − 2, nslab − 1 − sl) slabs, CPW instructions each (vmcnt counts in order)
   auto wait_slab = [&](int sl) {
     const int after = nslab - 1 - sl;
-    if (after >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    else if (after == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (after >= 2) {
+      if constexpr (X::CPW == 4) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    } else if (after == 1) {
+      if constexpr (X::CPW == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
   };
 
-  f32x16 run[2][2], cor[2][2], mprev[2][2];
+  f32x16 run[2][TQ], cor[2][TQ], mprev[2][TQ];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int j = 0; j < TQ; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r) run[i][j][r] = cor[i][j][r] = mprev[i][j][r] = 0.f;
   const f32x16 zero = {};
 
   const int kh = lane >> 5, li = lane & 31;
-  const bool live = q0 + wn * 64 < a.nq && (GATHER || e0 + wm * 64 < a.E);
+  const int wq0 = wn * 32 * TQ;  // this wave's first query column in the workgroup
+  const bool live = q0 + wq0 < a.nq && (GATHER || e0 + wm * 64 < a.E);
+  // the epilogue's exclusion-bitmap words, loaded now so their latency hides
+  // behind the K loop
+  uint32_t exw[TQ][2];
+#pragma unroll
+  for (int j = 0; j < TQ; ++j)
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int64_t q = q0 + wq0 + j * 32 + li;
+      const int64_t widx = (e0 >> 5) + wm * 2 + i;
+      const int64_t cbase = e0 + wm * 64 + i * 32;
+      uint32_t word = (!GATHER && q < a.nq && widx < a.W) ? a.fbits[q * a.W + widx] : ~0u;
+      const int64_t valid = a.E - cbase;
+      if (valid < 32) word |= (valid <= 0) ? ~0u : (~0u << valid);
+      exw[j][i] = word;
+    }
 #pragma unroll
   for (int p = 0; p < XS_NST - 1; ++p)
     if (p < nslab) issue(p, p);
   for (int sl = 0; sl < nslab; ++sl) {
-    wait_slab(sl);                // this wave's DMA of slab sl has landed
+    wait_slab(sl);                 // this wave's DMA of slab sl has landed
     __builtin_amdgcn_s_barrier();  // ... every wave's; slab sl-1's reads are done (no fence: the
                                    // vmcnt above covers the DMA, __syncthreads' would be vmcnt(0))
     if (sl + XS_NST - 1 < nslab) issue(sl + XS_NST - 1, (sl + XS_NST - 1) % XS_NST);
     if (!live || DIAG == 1) continue;
-    const uint16_t* Eh = smem + (sl % XS_NST) * 4 * XS_PIECE;
+    const uint16_t* Eh = smem + (sl % XS_NST) * X::STAGE;
     const uint16_t* El = Eh + XS_PIECE;
     const uint16_t* Qh = Eh + 2 * XS_PIECE;
-    const uint16_t* Ql = Eh + 3 * XS_PIECE;
-    bf16x8 eh[2], el[2], qh[2], ql[2];
+    const uint16_t* Ql = Qh + TQ * 1024;
+    bf16x8 eh[2], el[2], qh[TQ], ql[TQ];
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int row = wm * 64 + i * 32 + li;
@@ -479,18 +544,18 @@ __global__ __launch_bounds__(256, 2) void k_rank_mfma_x(XArgs a) {
       el[i] = *reinterpret_cast<const bf16x8*>(El + row * XS_BK + kh * 8);
     }
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int row = wn * 64 + j * 32 + li;
+    for (int j = 0; j < TQ; ++j) {
+      const int row = wq0 + j * 32 + li;
       qh[j] = *reinterpret_cast<const bf16x8*>(Qh + row * XS_BK + kh * 8);
       ql[j] = *reinterpret_cast<const bf16x8*>(Ql + row * XS_BK + kh * 8);
     }
     // the running sum takes the PREVIOUS slab's hi·hi products (long done:
     // an add right behind the MFMA it reads stalls the wave ~40 cycles), then
-    // this slab's four hi·hi and twelve correction MFMAs
+    // this slab's hi·hi and correction MFMAs
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
+      for (int j = 0; j < TQ; ++j) {
 #pragma unroll
         for (int r = 0; r < 16; r += 2) {
           f32x2 x = {run[i][j][r], run[i][j][r + 1]};
@@ -505,61 +570,73 @@ __global__ __launch_bounds__(256, 2) void k_rank_mfma_x(XArgs a) {
         cor[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(el[i], ql[j], cor[i][j], 0, 0, 0);
       }
   }
-  f32x16 acc[2][2];
+  f32x16 acc[2][TQ];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = (run[i][j] + mprev[i][j]) + cor[i][j];
+    for (int j = 0; j < TQ; ++j) acc[i][j] = (run[i][j] + mprev[i][j]) + cor[i][j];
 
   // C/D layout as the fp32 tile: col (query) = lane & 31, row (candidate) = (reg & 3) + 8·(reg >> 2) + 4·(lane >> 5)
   if (GATHER) {
-    if (wm != wn || kh != ((li >> 2) & 1)) return;
+    // query n's true row is candidate row n: wave wm = n / 64, tile i = (n % 64) / 32, row li
+    if (kh != ((li >> 2) & 1)) return;
     const int rd = 4 * (li >> 3) + (li & 3);
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int n = wn * 64 + i * 32 + li;
+    for (int j = 0; j < TQ; ++j) {
+      const int n = wq0 + j * 32 + li;
+      if ((n >> 6) != wm) continue;
+      const int i = (n & 63) >> 5;
 #pragma unroll
       for (int r = 0; r < 16; ++r)
-        if (r == rd && arow[n] >= 0) a.s_true[q0 + n] = acc[i][i][r];
+        if (r == rd && arow[n] >= 0) a.s_true[q0 + n] = (i == 0) ? acc[0][j][r] : acc[1][j][r];
     }
     return;
   }
-  const int64_t wbase = e0 >> 5;
+  if (DIAG == 3) {  // keep the accumulators live, skip the epilogue
+    float z = 0.f;
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int n = wn * 64 + j * 32 + li;
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < TQ; ++j) z += acc[i][j][0];
+    if (z == 12345.f) a.gt[0] = 1;
+    return;
+  }
+#pragma unroll
+  for (int j = 0; j < TQ; ++j) {
+    const int n = wq0 + j * 32 + li;
     const int64_t q = arow[n];
     const float st = sts[n], dlt = sdl[n];
-    uint32_t ex[2];
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int64_t widx = wbase + wm * 2 + i;
-      const int64_t cbase = e0 + wm * 64 + i * 32;
-      uint32_t word = (q >= 0 && widx < a.W) ? a.fbits[q * a.W + widx] : ~0u;
-      const int64_t valid = a.E - cbase;
-      if (valid < 32) word |= (valid <= 0) ? ~0u : (~0u << valid);
-      ex[i] = word;
-    }
+    const uint32_t ex[2] = {exw[j][0], exw[j][1]};
+    // branch-free count; the rare near-ties collect in a bit mask and are
+    // listed in one loop afterwards (a branch per candidate cost more than
+    // the count itself)
     int g = 0;
+    uint32_t near = 0;  // bit 16·i + r
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int mloc = (r & 3) + 8 * (r >> 2) + 4 * kh;
         const bool ok = ((ex[i] >> mloc) & 1u) == 0u;
-        const float sc = acc[i][j][r];
-        const float diff = sc - st;
+        const float diff = acc[i][j][r] - st;
         g += (ok && diff > dlt) ? 1 : 0;
-        if (ok && !(diff > dlt) && diff >= -dlt) {
-          const int idx = atomicAdd(&a.win.ucnt[q], 1);
-          if (idx < a.win.cap) a.win.ulist[q * (int64_t)a.win.cap + idx] = (int32_t)(e0 + wm * 64 + i * 32 + mloc);
-        }
+        near |= (ok && !(diff > dlt) && diff >= -dlt) ? (1u << (16 * i + r)) : 0u;
       }
+    if (__builtin_amdgcn_ballot_w64(near != 0u)) {
+      while (near) {
+        const int b = __builtin_ctz(near);
+        near &= near - 1u;
+        const int i = b >> 4, r = b & 15;
+        const int mloc = (r & 3) + 8 * (r >> 2) + 4 * kh;
+        const int idx = atomicAdd(&a.win.ucnt[q], 1);
+        if (idx < a.win.cap) a.win.ulist[q * (int64_t)a.win.cap + idx] = (int32_t)(e0 + wm * 64 + i * 32 + mloc);
+      }
+    }
     g += __shfl_xor(g, 32);
     if (kh == 0 && q >= 0 && g) atomicAdd(&cgt[n], g);
   }
   __syncthreads();
-  if (t < 128 && arow[t] >= 0 && cgt[t]) atomicAdd(&a.gt[q0 + t], cgt[t]);
+  if (t < X::BQ && arow[t] >= 0 && cgt[t]) atomicAdd(&a.gt[q0 + t], cgt[t]);
 }
 
 }  // namespace
@@ -624,27 +701,35 @@ int launch_rank_mfma_x(int gather, const uint16_t* qs, const uint16_t* es, int64
   if (qb >= XS_OOB || eb >= XS_OOB) return -1;  // 32-bit buffer offsets, XS_OOB reads zeros
   a.qs_bytes = (uint32_t)qb; a.es_bytes = (uint32_t)eb;
   a.true_id = true_id; a.s_true = s_true; a.fbits = bits; a.W = (E + 31) / 32; a.gt = gt; a.win = win;
-  const unsigned gy = (unsigned)((nq + BM - 1) / BM);
+  const char* tq_env = getenv("KGE_XTILE_TQ");  // query tiles per wave (A/B; default 2)
+  const int tq = (tq_env && atoi(tq_env) == 1) ? 1 : 2;
+  const int bq = 64 * tq;
+  const unsigned gy = (unsigned)((nq + bq - 1) / bq);
   a.gx = (int)((E + BN - 1) / BN);
   a.gy = (int)gy;
   // candidate tiles per L2 group: ≤ 2 MB of split rows (half an XCD's L2)
   const int64_t tile_bytes = (int64_t)BN * a.nslab * XS_BK * 4;
   a.group = (int)std::max<int64_t>(1, (2 << 20) / tile_bytes);
-  // __launch_bounds__(256, 2): 64 KB ring + 4.4 KB, ≤ 256 VGPRs — 2 workgroups = 2 waves per SIMD
+  if (const char* gg = getenv("KGE_XTILE_GROUP")) a.group = std::max(1, atoi(gg));
   if (gather) {
-    hipLaunchKernelGGL((k_rank_mfma_x<true>), dim3(1, gy), dim3(256), 0, s, a);
+    if (tq == 2) hipLaunchKernelGGL((k_rank_mfma_x<true, 2>), dim3(1, gy), dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((k_rank_mfma_x<true, 1>), dim3(1, gy), dim3(256), 0, s, a);
+    return (int)hipGetLastError();
+  }
+  const int64_t per_xcd = (int64_t)((a.gx + 7) / 8) * a.gy;  // XCD 0 has the most candidate tiles
+  const dim3 gs((unsigned)(8 * per_xcd));
+  const char* dg = getenv("KGE_XTILE_DIAG");  // timing diagnostics (tools/ab_rank.sh)
+  const int diag = dg ? atoi(dg) : 0;
+  if (tq == 1) {
+    hipLaunchKernelGGL((k_rank_mfma_x<false, 1>), gs, dim3(256), 0, s, a);
+  } else if (diag == 1) {
+    hipLaunchKernelGGL((k_rank_mfma_x<false, 2, 1>), gs, dim3(256), 0, s, a);
+  } else if (diag == 2) {
+    hipLaunchKernelGGL((k_rank_mfma_x<false, 2, 2>), gs, dim3(256), 0, s, a);
+  } else if (diag == 3) {
+    hipLaunchKernelGGL((k_rank_mfma_x<false, 2, 3>), gs, dim3(256), 0, s, a);
   } else {
-    const int64_t per_xcd = (int64_t)((a.gx + 7) / 8) * a.gy;  // XCD 0 has the most candidate tiles
-    const char* dg = getenv("KGE_XTILE_DIAG");  // timing diagnostics (tools/ab_rank)
-    const int diag = dg ? atoi(dg) : 0;
-    if (const char* gg = getenv("KGE_XTILE_GROUP")) a.group = std::max(1, atoi(gg));
-    const dim3 gs((unsigned)(8 * per_xcd));
-    if (diag == 1)
-      hipLaunchKernelGGL((k_rank_mfma_x<false, 1>), gs, dim3(256), 0, s, a);
-    else if (diag == 2)
-      hipLaunchKernelGGL((k_rank_mfma_x<false, 2>), gs, dim3(256), 0, s, a);
-    else
-      hipLaunchKernelGGL((k_rank_mfma_x<false>), gs, dim3(256), 0, s, a);
+    hipLaunchKernelGGL((k_rank_mfma_x<false, 2>), gs, dim3(256), 0, s, a);
   }
   return (int)hipGetLastError();
 }
