@@ -917,6 +917,10 @@ int kge_rank_filtered_ex(const kge_model_desc* m, int32_t mode, const int64_t* q
   if (st) return st;
   if (mode != KGE_HEAD_BATCH && mode != KGE_TAIL_BATCH) return KGE_ERR_MODE;
   if (!queries || !filt_off || !ranks_out || !err_flag || nq < 0) return KGE_ERR_ARG;
+  // KGE_RANK_REUSE_TABLE: the workspace already holds this entity table's
+  // statistics and split operands from the previous call (the other direction)
+  const bool reuse = (path & KGE_RANK_REUSE_TABLE) != 0;
+  path &= ~KGE_RANK_REUSE_TABLE;
   if (path < RP_AUTO || path > RP_MFMA32) return KGE_ERR_ARG;
   if (nq == 0) return KGE_OK;
   if (nq > 65535) return KGE_ERR_DIM;  // the bitmap launch puts queries on grid.y
@@ -955,7 +959,7 @@ int kge_rank_filtered_ex(const kge_model_desc* m, int32_t mode, const int64_t* q
   st = launch_status(launch_filter_bits(filt_off, filt_ids, w.true_id, nq, m->nentity, w.bits, err_flag, s));
   if (st) return st;
   if (m->model == KGE_DISTMULT || m->model == KGE_COMPLEX || m->model == KGE_PROTATE) {
-    st = launch_status(launch_table_stats(m->entity_embedding, m->nentity, m->entity_dim, w.stats, s));
+    if (!reuse) st = launch_status(launch_table_stats(m->entity_embedding, m->nentity, m->entity_dim, w.stats, s));
     if (st) return st;
   }
   // 3. the fast pass's own s_true (same instruction sequence as its candidates)
@@ -966,7 +970,8 @@ int kge_rank_filtered_ex(const kge_model_desc* m, int32_t mode, const int64_t* q
   ta.fbits = w.bits; ta.W = a.W; ta.gt = w.gt; ta.win = win;
   if (rp == RP_MFMA) {
     st = launch_status(launch_split_bf16(w.q, nq, m->entity_dim, w.qs, s));
-    if (!st) st = launch_status(launch_split_bf16(m->entity_embedding, m->nentity, m->entity_dim, w.es, s));
+    if (!st && !reuse)
+      st = launch_status(launch_split_bf16(m->entity_embedding, m->nentity, m->entity_dim, w.es, s));
     if (!st)
       st = launch_status(launch_rank_mfma_x(1, w.qs, w.es, nq, m->nentity, m->entity_dim, w.true_id, w.s_true,
                                             w.bits, w.gt, win, s));

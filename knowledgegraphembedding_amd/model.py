@@ -570,7 +570,7 @@ class KGEModel(nn.Module):
                 if qd is None:
                     qd, flat = flat[:3 * nq].view(nq, 3), flat[3 * nq:]
                 outs.append(ops.rank_filtered(self.desc(), mode, qd, flat[:nq + 1], flat[nq + 1:], dev, path=path,
-                                              relation_trig=trig))
+                                              relation_trig=trig, reuse_table=bool(outs)))
             # one device → host copy (pinned): both directions' ranks (int64 as
             # int32 pairs) and ties, and the error flag
             packed = torch.cat([outs[0][0].view(torch.int32), outs[1][0].view(torch.int32), outs[0][1], outs[1][1],

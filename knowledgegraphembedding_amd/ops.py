@@ -409,16 +409,22 @@ def reference_rotation(relation: torch.Tensor, embedding_range: float) -> torch.
     return torch.stack([torch.cos(phase), torch.sin(phase)], 1).contiguous()
 
 
+RANK_REUSE_TABLE = 0x100  # kge_hip.h KGE_RANK_REUSE_TABLE
+
+
 def rank_filtered(desc: _lib.ModelDesc, mode: str, queries: torch.Tensor, filt_off: torch.Tensor,
                   filt_ids: torch.Tensor, dev, path: str = "auto", listed: bool = False,
-                  relation_trig: Optional[torch.Tensor] = None):
+                  relation_trig: Optional[torch.Tensor] = None, reuse_table: bool = False):
     """Filtered ranks (int64) and tie counts (int32) for a block of queries
     (model.py:383-418), in the reference's fp32 score order
     (kge_rank_filtered_ex).  `path` picks the fast counting pass ("auto",
     "mfma" = split-bf16 MFMA tile, "mfma32" = fp32 MFMA tile, "tile", "scan"); `listed` also returns the per-query number of
     near-ties that were re-scored; `relation_trig` (RotatE, [R, 2, d] on the
     device, see reference_rotation) is the rotation table the ranks are
-    computed with (None: correctly rounded cos / sin)."""
+    computed with (None: correctly rounded cos / sin).  `reuse_table`: the
+    previous call on this device ranked the same model with the same entity
+    table (the other direction of one evaluation) — its table statistics and
+    split operands in the shared workspace are reused."""
     if mode not in ("head-batch", "tail-batch"):
         raise ValueError("mode %s not supported" % mode)
     if path not in RANK_PATHS:
@@ -443,7 +449,8 @@ def rank_filtered(desc: _lib.ModelDesc, mode: str, queries: torch.Tensor, filt_o
     ws = st.workspace(need)
     _lib.check(
         lib.kge_rank_filtered_ex(desc, _lib.MODE_IDS[mode], q.data_ptr(), nq, off.data_ptr(), ids.data_ptr(),
-                                 ranks.data_ptr(), ties.data_ptr(), _ptr(lst), RANK_PATHS[path], ws.data_ptr(),
+                                 ranks.data_ptr(), ties.data_ptr(), _ptr(lst),
+                                 RANK_PATHS[path] | (RANK_REUSE_TABLE if reuse_table else 0), ws.data_ptr(),
                                  ws.numel(), st.err.data_ptr(), _stream(dev)),
         "kge_rank_filtered_ex",
     )
