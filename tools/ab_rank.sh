@@ -1,7 +1,7 @@
 #!/bin/bash
 # A/B of the ranking tile under rocprofv3 kernel stats: one bench_rank run per
 # env-variant string, e.g.  tools/ab_rank.sh "KGE_XTILE_DIAG=0" "KGE_XTILE_DIAG=1"
-# Prints each variant's k_rank_mfma_x<false> min / mean launch time (µs).
+# Prints each variant's counting-tile min / max / mean launch time (µs).
 set -u
 ROOT="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 cd /tmp && export TMPDIR=/tmp
@@ -14,7 +14,8 @@ for v in "$@"; do
   python3 - "$OUT" "$v" <<'PY'
 import csv, sys
 for r in csv.DictReader(open(sys.argv[1] + "/run_kernel_stats.csv")):
-    if "k_rank_mfma_x<false" in r["Name"]:
-        print(sys.argv[2], "min", round(float(r["MinNs"]) / 1e3, 1), "mean", round(float(r["AverageNs"]) / 1e3, 1), "us")
+    if "k_rank_mfma_x<false" in r["Name"] or "k_rank_mfma_xp" in r["Name"]:
+        print(sys.argv[2], r["Name"][:40], "min", round(float(r["MinNs"]) / 1e3, 1), "max", round(float(r["MaxNs"]) / 1e3, 1),
+              "mean", round(float(r["AverageNs"]) / 1e3, 1), "us")
 PY
 done
