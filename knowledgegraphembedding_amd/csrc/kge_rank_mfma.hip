@@ -400,8 +400,8 @@ __device__ __forceinline__ bool xcd_tile(const XArgs& a, int& x, int& y) {
 // per wave, 133 VGPRs, a 48 KB ring, 3 workgroups per CU — more waves per SIMD
 // for 1.5× the fragment reads per MFMA and twice the candidate-tile DMAs;
 // measured equal (530 vs 523 µs, profiles/r03/rank/ab_tile_variants.txt).
-// DIAG (timing diagnostics only, wrong ranks; KGE_XTILE_DIAG): 1 = no MFMAs,
-// 2 = no LDS-DMA (MFMAs on whatever the ring holds), 3 = no epilogue.
+// (Timing diagnostics that dropped the MFMAs, the LDS-DMA or the epilogue —
+// measurements in profiles/r03/rank/ab_tile_variants.txt — are not in the tree.)
 template <int TQ>
 struct XTile {
   static constexpr int BQ = 64 * TQ;                   // queries per workgroup
@@ -409,7 +409,7 @@ struct XTile {
   static constexpr int CPW = 2 + TQ;                   // 1 KB DMA chunks per wave per slab
 };
 
-template <bool GATHER, int TQ, int DIAG = 0>
+template <bool GATHER, int TQ>
 __global__ __launch_bounds__(256, TQ == 1 ? 3 : 2) void k_rank_mfma_x(XArgs a) {
   using X = XTile<TQ>;
   // one LDS array: [XS_NST stages][E_hi | E_lo | Q_hi | Q_lo] then arow/brow, sts, sdl, cgt
@@ -455,7 +455,6 @@ __global__ __launch_bounds__(256, TQ == 1 ? 3 : 2) void k_rank_mfma_x(XArgs a) {
   const int64_t qrb = (int64_t)ty * X::BQ / 128;           // the queries' 128-row block in the split layout
   const uint32_t qsub = (uint32_t)((ty * X::BQ) & 127) * 32;  // … and their byte offset inside it
   auto issue = [&](int sl, int st) {
-    if (DIAG == 2) return;
     uint16_t* base = smem + st * X::STAGE;
 #pragma unroll
     for (int k = 0; k < X::CPW; ++k) {
@@ -531,7 +530,7 @@ __global__ __launch_bounds__(256, TQ == 1 ? 3 : 2) void k_rank_mfma_x(XArgs a) {
     __builtin_amdgcn_s_barrier();  // ... every wave's; slab sl-1's reads are done (no fence: the
                                    // vmcnt above covers the DMA, __syncthreads' would be vmcnt(0))
     if (sl + XS_NST - 1 < nslab) issue(sl + XS_NST - 1, (sl + XS_NST - 1) % XS_NST);
-    if (!live || DIAG == 1) continue;
+    if (!live) continue;
     const uint16_t* Eh = smem + (sl % XS_NST) * X::STAGE;
     const uint16_t* El = Eh + XS_PIECE;
     const uint16_t* Qh = Eh + 2 * XS_PIECE;
@@ -590,15 +589,6 @@ __global__ __launch_bounds__(256, TQ == 1 ? 3 : 2) void k_rank_mfma_x(XArgs a) {
       for (int r = 0; r < 16; ++r)
         if (r == rd && arow[n] >= 0) a.s_true[q0 + n] = (i == 0) ? acc[0][j][r] : acc[1][j][r];
     }
-    return;
-  }
-  if (DIAG == 3) {  // keep the accumulators live, skip the epilogue
-    float z = 0.f;
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < TQ; ++j) z += acc[i][j][0];
-    if (z == 12345.f) a.gt[0] = 1;
     return;
   }
 #pragma unroll
@@ -718,19 +708,10 @@ int launch_rank_mfma_x(int gather, const uint16_t* qs, const uint16_t* es, int64
   }
   const int64_t per_xcd = (int64_t)((a.gx + 7) / 8) * a.gy;  // XCD 0 has the most candidate tiles
   const dim3 gs((unsigned)(8 * per_xcd));
-  const char* dg = getenv("KGE_XTILE_DIAG");  // timing diagnostics (tools/ab_rank.sh)
-  const int diag = dg ? atoi(dg) : 0;
-  if (tq == 1) {
+  if (tq == 1)
     hipLaunchKernelGGL((k_rank_mfma_x<false, 1>), gs, dim3(256), 0, s, a);
-  } else if (diag == 1) {
-    hipLaunchKernelGGL((k_rank_mfma_x<false, 2, 1>), gs, dim3(256), 0, s, a);
-  } else if (diag == 2) {
-    hipLaunchKernelGGL((k_rank_mfma_x<false, 2, 2>), gs, dim3(256), 0, s, a);
-  } else if (diag == 3) {
-    hipLaunchKernelGGL((k_rank_mfma_x<false, 2, 3>), gs, dim3(256), 0, s, a);
-  } else {
+  else
     hipLaunchKernelGGL((k_rank_mfma_x<false, 2>), gs, dim3(256), 0, s, a);
-  }
   return (int)hipGetLastError();
 }
 

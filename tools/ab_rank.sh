@@ -1,6 +1,6 @@
 #!/bin/bash
 # A/B of the ranking tile under rocprofv3 kernel stats: one bench_rank run per
-# env-variant string, e.g.  tools/ab_rank.sh "KGE_XTILE_DIAG=0" "KGE_XTILE_DIAG=1"
+# env-variant string, e.g.  tools/ab_rank.sh "KGE_XTILE_TQ=2" "KGE_XTILE_TQ=1"
 # Prints each variant's counting-tile min / max / mean launch time (µs).
 set -u
 ROOT="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
