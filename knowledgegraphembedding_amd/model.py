@@ -300,6 +300,7 @@ class KGEModel(nn.Module):
         pos = pos.to(dev)
         neg = None if neg is None else neg.to(dev)
         g, rng = self._host_scalars()
+        torch_ops.load()
         return torch.ops.kge.score(self.entity_embedding, self.relation_embedding, pos, neg, _lib.MODE_IDS[mode],
                                    _lib.MODEL_IDS[self.model_name], g, rng, self._modulus())
 
@@ -328,6 +329,7 @@ class KGEModel(nn.Module):
         else:
             raise ValueError('mode %s not supported' % mode)
         g, rng = self._host_scalars()
+        torch_ops.load()
         return torch.ops.kge.score(ent.contiguous(), relation.reshape(B, -1).contiguous(), pos, neg,
                                    _lib.MODE_IDS[mode], _lib.MODEL_IDS[name], g, rng, self._modulus())
 

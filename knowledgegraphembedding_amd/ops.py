@@ -55,7 +55,8 @@ class _DeviceState:
         self.dev = dev
         self.ws = {}
         # the flag the torch.ops.kge.* kernels OR into too (one per device)
-        from . import torch_ops  # noqa: F401  (loads libkge_torch.so)
+        from . import torch_ops
+        torch_ops.load()
         self.err = torch.ops.kge.error_flag(dev)
 
     def workspace(self, nbytes: int) -> torch.Tensor:

@@ -48,7 +48,8 @@ _LOADED = [False]
 
 
 def load() -> None:
-    """Register torch.ops.kge.* from libkge_torch.so (once), or raise."""
+    """Register torch.ops.kge.* from libkge_torch.so (once), or raise: every
+    entry point of the package calls this before its first torch.ops.kge op."""
     if _LOADED[0]:
         return
     if not LIB_PATH.exists():
@@ -58,4 +59,7 @@ def load() -> None:
     _LOADED[0] = True
 
 
-load()
+# registered at import when built; a fresh checkout can still be imported to
+# build it (`build.py` imports the package), and its first op raises above
+if LIB_PATH.exists():
+    load()
