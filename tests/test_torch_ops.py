@@ -4,6 +4,8 @@ CPU: the schemas are registered and the Meta kernels give the right output
 metadata, so torch.compile / fake-tensor tracing can carry the ops without
 running them; argument errors raise the reference's ValueErrors and CPU
 tensors are refused (no CPU path).  The GPU half is tests/test_torch_ops_gpu.py."""
+import os
+
 import pytest
 import torch
 from torch._subclasses.fake_tensor import FakeTensorMode
@@ -61,3 +63,32 @@ def test_reference_errors_and_no_cpu_path():
     with pytest.raises(RuntimeError, match="ROCm"):
         torch.ops.kge.rank_filtered(ent, rel, None, pos, torch.zeros(3, dtype=torch.int64),
                                     torch.zeros(0, dtype=torch.int64), TAIL, ROTATE, 12.0, 0.5)
+
+
+def test_unbuilt_checkout_imports_and_fails_loudly_at_first_op():
+    """A checkout without the built libraries must still import (build.py
+    imports the package to build it), and the first op must raise — there is
+    no CPU or Python fallback."""
+    import subprocess
+    import sys
+    code = (
+        "import torch\n"
+        "import knowledgegraphembedding_amd as k\n"
+        "from knowledgegraphembedding_amd import torch_ops, _lib\n"
+        "try:\n"
+        "    torch_ops.load()\n"
+        "except RuntimeError as e:\n"
+        "    assert 'missing' in str(e)\n"
+        "else:\n"
+        "    raise SystemExit('torch_ops.load() did not raise')\n"
+        "try:\n"
+        "    _lib.load()\n"
+        "except RuntimeError as e:\n"
+        "    assert 'missing' in str(e)\n"
+        "else:\n"
+        "    raise SystemExit('_lib.load() did not raise')\n"
+        "print('ok')\n")
+    env = dict(os.environ, KGE_TORCH_LIB="/nonexistent/libkge_torch.so", KGE_HIP_LIB="/nonexistent/libkge_hip.so")
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300,
+                       cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stdout + r.stderr
