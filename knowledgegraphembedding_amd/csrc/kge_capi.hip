@@ -891,9 +891,10 @@ RankWs carve_rank(void* ws, const kge_model_desc* m, int64_t nq, size_t* bytes) 
   w.ucnt = w.gt ? w.gt + 4 * nq : nullptr;
   w.ulist = c.take<int32_t>(nq * (int64_t)RANK_CAP);
   w.bits = c.take<uint32_t>(nq * ((m->nentity + 31) / 32));
-  const bool bil = (m->model == KGE_DISTMULT || m->model == KGE_COMPLEX);
-  w.qs = c.take<uint16_t>(bil ? xsplit_elems(nq, m->entity_dim) : 0);
-  w.es = c.take<uint16_t>(bil ? xsplit_elems(m->nentity, m->entity_dim) : 0);
+  // split-bf16 operands: only where the split tile can run (rank_path's x_ok)
+  const bool xs = rank_path(m, RP_MFMA) == RP_MFMA;
+  w.qs = c.take<uint16_t>(xs ? xsplit_elems(nq, m->entity_dim) : 0);
+  w.es = c.take<uint16_t>(xs ? xsplit_elems(m->nentity, m->entity_dim) : 0);
   *bytes = c.off + 256;
   return w;
 }
