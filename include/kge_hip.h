@@ -414,10 +414,11 @@ int kge_rank_filtered(const kge_model_desc *m, int32_t mode, const int64_t *quer
  * listed_out [nq] int32 (nullable): near-ties re-scored per query (above the
  * 1024-per-query list capacity the query is rescanned exactly).  Every path
  * returns the same ranks and ties.  path | KGE_RANK_REUSE_TABLE: the caller
- * asserts that the previous call on this same workspace and stream ranked the
- * same number of queries with the same model and an unchanged entity table
- * (the other direction of one evaluation), so the table's statistics and
- * split operands are reused.
+ * asserts that an earlier call on this same workspace (same pointer, not
+ * written in between, stream-ordered before this one) ranked with the same
+ * model and an unchanged entity table — the other direction or another query
+ * block of one evaluation, any nq — so the table's statistics and split
+ * operands it left at the start of the workspace are reused.
  */
 #define KGE_RANK_REUSE_TABLE 0x100
 int kge_rank_filtered_ex(const kge_model_desc *m, int32_t mode, const int64_t *queries, int64_t nq,

@@ -877,24 +877,26 @@ struct RankWs {
 RankWs carve_rank(void* ws, const kge_model_desc* m, int64_t nq, size_t* bytes) {
   Carver c(ws);
   RankWs w;
+  // the entity table's own buffers first, at offsets independent of nq, so a
+  // later call on the same workspace can reuse them (KGE_RANK_REUSE_TABLE)
+  w.stats = c.take<float>(2 + 2 * TS_BLOCKS);  // [max ‖e‖, max |x|, per-block partials]
+  // split-bf16 operands: only where the split tile can run (rank_path's x_ok)
+  const bool xs = rank_path(m, RP_MFMA) == RP_MFMA;
+  w.es = c.take<uint16_t>(xs ? xsplit_elems(m->nentity, m->entity_dim) : 0);
+  w.qs = c.take<uint16_t>(xs ? xsplit_elems(nq, m->entity_dim) : 0);
   w.q = c.take<float>(nq * (int64_t)m->entity_dim);
   w.qref = c.take<float>(nq * (int64_t)m->entity_dim);
   w.s_true = c.take<float>(nq);
   w.sref_true = c.take<float>(nq);
   w.delta = c.take<float>(nq);
-  w.stats = c.take<float>(2 + 2 * TS_BLOCKS);  // [max ‖e‖, max |x|, per-block partials]
   w.true_id = c.take<int64_t>(nq);
-  w.gt = c.take<int32_t>(5 * nq);  // gt, eq, gtx, eqx, ucnt: one memset
+  w.gt = c.take<int32_t>(5 * nq);  // gt, eq, gtx, eqx, ucnt (zeroed by k_rank_prep)
   w.eq = w.gt ? w.gt + nq : nullptr;
   w.gtx = w.gt ? w.gt + 2 * nq : nullptr;
   w.eqx = w.gt ? w.gt + 3 * nq : nullptr;
   w.ucnt = w.gt ? w.gt + 4 * nq : nullptr;
   w.ulist = c.take<int32_t>(nq * (int64_t)RANK_CAP);
   w.bits = c.take<uint32_t>(nq * ((m->nentity + 31) / 32));
-  // split-bf16 operands: only where the split tile can run (rank_path's x_ok)
-  const bool xs = rank_path(m, RP_MFMA) == RP_MFMA;
-  w.qs = c.take<uint16_t>(xs ? xsplit_elems(nq, m->entity_dim) : 0);
-  w.es = c.take<uint16_t>(xs ? xsplit_elems(m->nentity, m->entity_dim) : 0);
   *bytes = c.off + 256;
   return w;
 }

@@ -523,7 +523,8 @@ class KGEModel(nn.Module):
                     q = triples[b0:b0 + block]
                     off, ids = index.filter_csr(q, mode)
                     ranks, _ = ops.rank_filtered(desc, mode, torch.from_numpy(q), torch.from_numpy(off),
-                                                 torch.from_numpy(ids), dev, relation_trig=trig)
+                                                 torch.from_numpy(ids), dev, relation_trig=trig,
+                                                 reuse_table=step > 0)
                     ranks_all.append(ranks)
                     # progress messages on the reference's batch cadence
                     nb = (len(q) + test_batch_size - 1) // test_batch_size

@@ -54,12 +54,14 @@ class _DeviceState:
     def __init__(self, dev: torch.device):
         self.dev = dev
         self.ws = {}
+        self.rank_ws_ptr = 0  # workspace of the last ranking call (KGE_RANK_REUSE_TABLE)
         # the flag the torch.ops.kge.* kernels OR into too (one per device)
         from . import torch_ops
         torch_ops.load()
         self.err = torch.ops.kge.error_flag(dev)
 
     def workspace(self, nbytes: int) -> torch.Tensor:
+        self.rank_ws_ptr = 0  # any user may overwrite the ranking's reusable table buffers
         s = torch.cuda.current_stream(self.dev)
         key = s.cuda_stream
         ws = self.ws.get(key)
@@ -422,10 +424,11 @@ def rank_filtered(desc: _lib.ModelDesc, mode: str, queries: torch.Tensor, filt_o
     "mfma" = split-bf16 MFMA tile, "mfma32" = fp32 MFMA tile, "tile", "scan"); `listed` also returns the per-query number of
     near-ties that were re-scored; `relation_trig` (RotatE, [R, 2, d] on the
     device, see reference_rotation) is the rotation table the ranks are
-    computed with (None: correctly rounded cos / sin).  `reuse_table`: the
-    previous call on this device ranked the same model with the same entity
-    table (the other direction of one evaluation) — its table statistics and
-    split operands in the shared workspace are reused."""
+    computed with (None: correctly rounded cos / sin).  `reuse_table`: an
+    earlier call on this device ranked the same model with the same, unchanged
+    entity table (the other direction or another query block of one
+    evaluation) — its table statistics and split operands are reused when the
+    shared workspace is still the same buffer (else recomputed)."""
     if mode not in ("head-batch", "tail-batch"):
         raise ValueError("mode %s not supported" % mode)
     if path not in RANK_PATHS:
@@ -447,7 +450,11 @@ def rank_filtered(desc: _lib.ModelDesc, mode: str, queries: torch.Tensor, filt_o
     lib = _lib.load()
     need = lib.kge_rank_workspace_bytes(desc, nq)
     st = state(dev)
+    prev = st.rank_ws_ptr  # the last ranking call's buffer, cleared by any other workspace user
     ws = st.workspace(need)
+    # the table's statistics / split operands survive only in the same buffer
+    reuse_table = reuse_table and prev == ws.data_ptr()
+    st.rank_ws_ptr = ws.data_ptr()
     _lib.check(
         lib.kge_rank_filtered_ex(desc, _lib.MODE_IDS[mode], q.data_ptr(), nq, off.data_ptr(), ids.data_ptr(),
                                  ranks.data_ptr(), ties.data_ptr(), _ptr(lst),

@@ -106,3 +106,36 @@ def test_rank_queries_both_directions_pipelined(name):
     rt1, tt1 = m.rank_queries(q, true, "tail-batch")
     assert np.array_equal(rh, rh1) and np.array_equal(th, th1)
     assert np.array_equal(rt, rt1) and np.array_equal(tt, tt1)
+
+
+@pytest.mark.parametrize("name", ["DistMult", "ComplEx"])
+def test_test_step_query_blocks_reuse_the_table(name):
+    """test_step ranks in query blocks of at most 16384 and, from the second
+    block (and direction) on, reuses the table statistics and split operands
+    the first call left in the workspace (KGE_RANK_REUSE_TABLE); its ranks
+    must equal one unblocked rank_queries call per direction without reuse.
+    A training step between two evaluations must drop the reuse (the step
+    writes the shared workspace and the table)."""
+    E, R, d = 300, 7, 24
+    m, *_ = build_model(name, E, R, d, 12.0, 9)
+    g = np.random.default_rng(4)
+    test = np.stack([g.integers(0, E, 20000), g.integers(0, R, 20000), g.integers(0, E, 20000)], 1).astype(np.int64)
+    true = np.unique(test, axis=0)
+    args = Namespace(countries=False, nentity=E, nrelation=R, test_batch_size=16, cpu_num=2, test_log_steps=10 ** 9,
+                     cuda=True, negative_adversarial_sampling=True, adversarial_temperature=1.0, uni_weight=False,
+                     regularization=0.0)
+
+    def expected():
+        ranks = np.concatenate([m.rank_queries(test, true, mode)[0] for mode in ("head-batch", "tail-batch")])
+        return float(np.mean(1.0 / ranks)), float(np.mean(ranks))
+
+    for rnd in range(2):
+        met = KGEModel.test_step(m, [tuple(x) for x in test.tolist()], [tuple(x) for x in true.tolist()], args)
+        mrr, mr = expected()
+        assert abs(met["MRR"] - mrr) < 1e-9 and abs(met["MR"] - mr) < 1e-6, (rnd, met, mrr, mr)
+        # one training step changes the table before the next evaluation
+        pos, neg, w = synth.kge_batch(50 + rnd, 32, 16, E, R)
+        m.compute_train_grads(torch.from_numpy(pos).to(DEV), torch.from_numpy(neg).to(DEV),
+                              torch.from_numpy(w).to(DEV), "tail-batch", args)
+        with torch.no_grad():
+            m.entity_embedding.add_(m.entity_embedding.grad, alpha=-100.0)
