@@ -391,6 +391,16 @@ def main():
         ceiling = {"GBps": c0["GBps"], "frac": achieved / c0["GBps"], "source": "profiles/r01/gather_ceiling.jsonl",
                    "what": "same grid and buffer loads over the same table, no arithmetic"}
 
+    ent_ceiling = None  # the entity pass's HBM stream alone (tools/dbg/stream_ceiling.hip), measured on MI355X
+    sj = os.path.join(here, "profiles", "entity_stream_ceiling.jsonl")
+    if a.workload == "fb15k" and os.path.exists(sj) and ent_achieved:
+        with open(sj) as f:
+            best = max((json.loads(line) for line in f if line.strip()), key=lambda r: r["GBps"])
+        ent_ceiling = {"GBps": best["GBps"], "frac": ent_achieved / best["GBps"],
+                       "source": "profiles/entity_stream_ceiling.jsonl",
+                       "what": "the dense Adam stream alone (read p/m/v, write p/m/v/grad, 837 MB, coalesced, "
+                               "non-temporal), without the entity pass's 2.1 GB of q-slice gathers from L2"}
+
     value = a.steps * B * (NNEG + 1) * world / dt
     out = {
         "metric": METRIC,
@@ -425,7 +435,8 @@ def main():
         "roofline_entity": {"bound": "hbm", "kernel": "k_entity_sl (entity-major gradient + fused Adam; relation rows in trailing blocks)",
                             "achieved": ent_achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                             "frac": ent_achieved / HBM_PEAK_GBS if ent_achieved else None, "traffic": ent_traffic,
-                            "algorithmic_bytes_per_launch": ent_bytes, "avg_launch_ms": ent_ms},
+                            "algorithmic_bytes_per_launch": ent_bytes, "avg_launch_ms": ent_ms,
+                            "pattern_ceiling": ent_ceiling},
         "step_roofline": None if exchanged else step_roofline(dt / a.steps, row_bytes, ent_bytes, row_traffic,
                                                                  ent_traffic),
     }
