@@ -155,6 +155,11 @@ struct StageTimer {
     }
     return ev[used++];
   }
+  hipEvent_t dbg = nullptr;
+  void marker(hipStream_t s) {  // KGE_DBG_EVENTS: an untimed event record, as the side-stream fork is
+    if (!dbg && hipEventCreateWithFlags(&dbg, hipEventDisableTiming) != hipSuccess) return;
+    hipEventRecord(dbg, s);
+  }
   void mark(hipStream_t s) {
     if (!on) return;
     hipEvent_t e = next(s);
@@ -335,12 +340,35 @@ int run_grad(const kge_model_desc* m, const Geom& geo, int mode, const int64_t* 
     for (int k = 0; k < 3; ++k) g_timer.mark(s);  // stages 3-5 not in this call
   }  // KGE_PHASE_ROWS
 
+  fa.row_stats = w.row_stats;
+  fa.reg_partial = (reg != 0.f) ? w.reg_partial : nullptr;
+  {
+    // entity rows [e_begin, e_end) (all of them unless an owner's range) and,
+    // unless the caller counts them elsewhere, the relation rows
+    const int64_t per = ent_parts / (m->nentity > 0 ? m->nentity : 1);
+    fa.reg_a0 = e_begin * per;
+    fa.reg_a1 = e_end * per;
+    fa.reg_b0 = ent_parts;
+    fa.reg_b1 = ent_parts + (reg_relations ? m->nrelation : 0);
+  }
+  fa.regularization = reg;
+  fa.grad_modulus = grad_modulus;
+  fa.adam = adam_t((adam && m->model == KGE_PROTATE) ? &adam->modulus : nullptr);
+  fa.adamk = ak;
+  // the loss finalisation rides in the entity launch's last block when that
+  // launch is the whole rest of the step and writes nothing the finalisation
+  // reads (no regulariser partials, no pRotatE modulus update)
+  const bool fin_wanted = (phases & KGE_PHASE_FINALIZE) && (fa.losses || grad_modulus);
+  const bool fin_fused = fin_wanted && all && rel_fused && e_end > e_begin && !fa.reg_partial && !fa.adam.p &&
+                         env_int("KGE_FIN_SEPARATE", 0) == 0;
+
   if (phases & KGE_PHASE_ENTITY) {
   if (sd && !csr_ready)
     hipStreamWaitEvent(s, sd->csr_done, 0);  // join 1: the entity pass reads the CSR
   if (timed) g_timer.mark(s);
 
   EntArgs ea;
+  memset(&ea, 0, sizeof(ea));
   ea.ent = m->entity_embedding; ea.modulus = m->modulus; ea.E = m->nentity; ea.Le = Le; ea.eg = geo.eg;
   ea.e_begin = e_begin; ea.e_end = e_end;
   ea.c = c; ea.off = w.off; ea.occ = w.occ; ea.Bn = B * n; ea.n = n;
@@ -356,6 +384,8 @@ int run_grad(const kge_model_desc* m, const Geom& geo, int mode, const int64_t* 
   ea.rel = rl;
   ea.B = B;
   ea.rel_blocks = rel_fused ? (m->nrelation + 3) / 4 : 0;
+  ea.fin = fa;
+  ea.fin_fused = fin_fused ? 1 : 0;
   if (e_end > e_begin) {
     st = launch_status(op.entity(mode, geo.vec, geo.ns, ea, s));
     if (st) return st;
@@ -375,22 +405,8 @@ int run_grad(const kge_model_desc* m, const Geom& geo, int mode, const int64_t* 
     st = launch_status(launch_rel_rows(rl, s));
     if (st) return st;
   }
-  fa.row_stats = w.row_stats;
-  fa.reg_partial = (reg != 0.f) ? w.reg_partial : nullptr;
-  {
-    // entity rows [e_begin, e_end) (all of them unless an owner's range) and,
-    // unless the caller counts them elsewhere, the relation rows
-    const int64_t per = ent_parts / (m->nentity > 0 ? m->nentity : 1);
-    fa.reg_a0 = e_begin * per;
-    fa.reg_a1 = e_end * per;
-    fa.reg_b0 = ent_parts;
-    fa.reg_b1 = ent_parts + (reg_relations ? m->nrelation : 0);
-  }
-  fa.regularization = reg;
-  fa.grad_modulus = grad_modulus;
-  fa.adam = adam_t((adam && m->model == KGE_PROTATE) ? &adam->modulus : nullptr);
-  fa.adamk = ak;
-  if (fa.losses || grad_modulus) {
+  for (int k = env_int("KGE_DBG_EVENTS", 0); k > 0; --k) g_timer.marker(s);  // diagnostic: cost of a marker
+  if (fin_wanted && !fin_fused) {
     st = launch_status(launch_finalize(fa, s));
     if (st) return st;
   }

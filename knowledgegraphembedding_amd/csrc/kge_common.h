@@ -21,22 +21,6 @@ struct CsrArgs {
 };
 
 
-struct FinArgs {
-  const float* row_stats;    // [B, 4]
-  const float* sub_w;        // nullable
-  const float* w_sum;        // nullable → Σ of sub_w
-  int64_t B;
-  int uni_weight;
-  float uni_n;               // global batch size (uni_weight means)
-  const float* reg_partial;  // or null; summed over [reg_a0, reg_a1) then [reg_b0, reg_b1)
-  int64_t reg_a0, reg_a1, reg_b0, reg_b1;  // (entity parts, relation rows; a sub-range for an owner's step)
-  float regularization;
-  float* losses;             // [4]
-  float* grad_modulus;       // nullable
-  const int32_t* err;        // device error flag, copied to losses[4]
-  AdamT adam;                // fused optimizer step of the pRotatE modulus (adam.p == null: none)
-  AdamK adamk;
-};
 
 int launch_rank_mfma(int gather, const float* q, const float* ent, int64_t nq, int64_t E, int K,
                      const int64_t* true_id, float* s_true, const uint32_t* bits, int32_t* gt, const RankWin& win,

@@ -90,76 +90,10 @@ __global__ __launch_bounds__(256) void k_rel_rows(RelArgs a) {
 
 // ------------------------------------------------------------ finalise
 // Loss scalars (model.py:279-297) and d/dmodulus.  One workgroup, fixed
-// reduction order.
+// reduction order (finalize_block, kge_rel.h).
 __global__ __launch_bounds__(1024) void k_finalize(FinArgs a) {
-  __shared__ float red[6][1024];
-  const int tid = threadIdx.x;
-  float sw = 0.f, swp = 0.f, swn = 0.f, sp = 0.f, sn = 0.f, mg = 0.f;
-  for (int64_t i = tid; i < a.B; i += 1024) {
-    const float* st = a.row_stats + i * 4;
-    const float w = a.sub_w ? a.sub_w[i] : 1.f;
-    sw += w;
-    swp += w * st[0];
-    swn += w * st[1];
-    sp += st[0];
-    sn += st[1];
-    mg += st[2];
-  }
-  red[0][tid] = sw; red[1][tid] = swp; red[2][tid] = swn;
-  red[3][tid] = sp; red[4][tid] = sn; red[5][tid] = mg;
-  __syncthreads();
-  for (int o = 512; o > 0; o >>= 1) {
-    if (tid < o)
-      for (int u = 0; u < 6; ++u) red[u][tid] += red[u][tid + o];
-    __syncthreads();
-  }
-  float tot[6];
-#pragma unroll
-  for (int u = 0; u < 6; ++u) tot[u] = red[u][0];
-  float reg = 0.f;
-  const int64_t na = a.reg_a1 - a.reg_a0, nreg = na + (a.reg_b1 - a.reg_b0);
-  if (a.reg_partial && nreg > 0) {
-    float s = 0.f;
-    for (int64_t v = tid; v < nreg; v += 1024) s += a.reg_partial[v < na ? a.reg_a0 + v : a.reg_b0 + (v - na)];
-    __syncthreads();
-    red[0][tid] = s;
-    __syncthreads();
-    for (int o = 512; o > 0; o >>= 1) {
-      if (tid < o) red[0][tid] += red[0][tid + o];
-      __syncthreads();
-    }
-    reg = a.regularization * red[0][0];
-  }
-  if (tid == 0) {
-    float pos_loss, neg_loss;
-    if (a.uni_weight) {
-      // - score.mean(): sum / batch  (model.py:282-283)
-      pos_loss = -(tot[3] / a.uni_n);
-      neg_loss = -(tot[4] / a.uni_n);
-    } else {
-      // - (w * score).sum() / w.sum()  (model.py:285-286)
-      const float wsum = a.w_sum ? a.w_sum[0] : tot[0];
-      pos_loss = -(tot[1] / wsum);
-      neg_loss = -(tot[2] / wsum);
-    }
-    float loss = (pos_loss + neg_loss) / 2.f;
-    loss = loss + reg;
-    if (a.losses) {
-      a.losses[0] = pos_loss;
-      a.losses[1] = neg_loss;
-      a.losses[2] = loss;
-      a.losses[3] = reg;
-      // the device error flag rides along, so the caller's one read-back of
-      // the losses also tells it whether any index was out of range
-      a.losses[4] = a.err ? (float)__hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.f;
-    }
-    if (a.grad_modulus) a.grad_modulus[0] = tot[5];
-    if (a.adam.p) {  // pRotatE modulus, fused optimizer step
-      float pv = a.adam.p[0], mv = a.adam.m[0], vv = a.adam.v[0];
-      adam_elem(pv, tot[5], mv, vv, a.adamk, a.adam.step_size, a.adam.bc2s);
-      a.adam.p[0] = pv; a.adam.m[0] = mv; a.adam.v[0] = vv;
-    }
-  }
+  __shared__ float red[6 * 1024];
+  finalize_block<1024>(a, red);
 }
 
 // Same fixed order as k_row's / k_build_q's in-kernel Σw (block_weight_sum,

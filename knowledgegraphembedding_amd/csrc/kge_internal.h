@@ -97,6 +97,24 @@ struct RelArgs {
   AdamK adamk;
 };
 
+// Loss finalisation (k_finalize, or the entity launch's last block: EntArgs.fin)
+struct FinArgs {
+  const float* row_stats;    // [B, 4]
+  const float* sub_w;        // nullable
+  const float* w_sum;        // nullable → Σ of sub_w
+  int64_t B;
+  int uni_weight;
+  float uni_n;               // global batch size (uni_weight means)
+  const float* reg_partial;  // or null; summed over [reg_a0, reg_a1) then [reg_b0, reg_b1)
+  int64_t reg_a0, reg_a1, reg_b0, reg_b1;  // (entity parts, relation rows; a sub-range for an owner's step)
+  float regularization;
+  float* losses;             // [4]
+  float* grad_modulus;       // nullable
+  const int32_t* err;        // device error flag, copied to losses[4]
+  AdamT adam;                // fused optimizer step of the pRotatE modulus (adam.p == null: none)
+  AdamK adamk;
+};
+
 struct EntArgs {
   const float* ent;
   const float* modulus;
@@ -124,6 +142,8 @@ struct EntArgs {
   AdamK adamk;
   RelArgs rel;          // rel_blocks > 0: trailing blocks of k_entity_sl run the relation pass
   int64_t rel_blocks;
+  FinArgs fin;          // fin_fused: the launch's last block runs the loss finalisation
+  int fin_fused;        // (only when nothing it reads is written by this launch)
 };
 
 // Near-tie window of the fast ranking passes (all three): a candidate whose

@@ -250,6 +250,36 @@ def test_fused_adam_bitwise_equals_unfused(name):
         assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("name,uni,B", [("RotatE", False, 1500), ("RotatE", True, 300), ("TransE", False, 64),
+                                         ("pRotatE", False, 200), ("ComplEx", True, 1100)])
+def test_fused_finalize_bitwise_equals_separate(name, uni, B, monkeypatch):
+    """The loss finalisation in the entity launch's last block (256 threads)
+    folds its sums in k_finalize's 1024-thread order: losses, modulus gradient
+    and the fused Adam state are bit-identical with KGE_FIN_SEPARATE=1 (the
+    separate k_finalize launch), for batches below, between and above the
+    workgroup widths."""
+    E, R, d, n = 900, 9, 64, 24
+    pos, neg, w = synth.kge_batch(5, B, n, E, R)
+    P, N, W = torch.from_numpy(pos).to(DEV), torch.from_numpy(neg).to(DEV), torch.from_numpy(w).to(DEV)
+    args = Namespace(negative_adversarial_sampling=True, adversarial_temperature=0.7, uni_weight=uni,
+                     regularization=0.0)
+    runs = []
+    for sep in ("0", "1"):
+        monkeypatch.setenv("KGE_FIN_SEPARATE", sep)
+        m, *_ = build_model(name, E, R, d, 12.0, 17)
+        opt = KGEAdam([p for p in m.parameters() if p.requires_grad], lr=3e-3)
+        out = []
+        for step, mode in enumerate(("tail-batch", "head-batch", "tail-batch")):
+            fused_opt = opt if step > 0 else None  # one plain step (grads + k_finalize's twin), then fused Adam
+            out.append(m.compute_train_grads(P, N, W, mode, args, optimizer=fused_opt).cpu().clone())
+            if fused_opt is None:
+                opt.step()
+        out += [t.detach().cpu().clone() for t in m.parameters()]
+        runs.append(out)
+    for a, b in zip(*runs):
+        assert torch.equal(a, b)
+
+
 @pytest.mark.parametrize("name", NAMES)
 def test_phased_step_bitwise_equals_single_call(name):
     """kge_train_step_grads_phased (rows, entity-row chunks in any order,
