@@ -224,6 +224,27 @@ int entity_slices(const Geom& geo, int64_t B, int Le) {
   return ((k == 1 || k == 2 || k == 4 || k == 8) && fits(k)) ? k : 0;
 }
 
+// Line-aligned slicing for k_entity_sl (align_sl): the inner slice boundaries
+// of a row move by the row's 16-B phase within its 128-B line so they fall on
+// line boundaries of the row's first half.  Only when every stream of the pass
+// (table = Adam param, gradient, moments) has the same phase, every row's
+// phase is one the 64-slot slices absorb (last slice ≤ 64 slots) — d = 1000:
+// phases 0 and 4 — and KGE_ENT_ALIGN is not 0.
+int entity_slice_align(int nsl, int S, int Le, const float* ent, const float* grad, const AdamT& ad) {
+  if (nsl < 2 || env_int("KGE_ENT_ALIGN", 1) == 0) return 0;
+  const uintptr_t base = (uintptr_t)ent & 127;
+  if (base & 15) return 0;
+  for (const float* p : {grad, (const float*)ad.p, (const float*)ad.m, (const float*)ad.v})
+    if (p && ((uintptr_t)p & 127) != base) return 0;
+  if (S <= 64 * (nsl - 1)) return 0;
+  int max_sh = 0;
+  for (int e = 0; e < 8; ++e) {
+    const int sh = (int)(((base + (uintptr_t)e * (uintptr_t)Le * 4u) >> 4) & 7);
+    max_sh = sh > max_sh ? sh : max_sh;
+  }
+  return (S - 64 * (nsl - 1) + max_sh <= 64) ? 1 : 0;
+}
+
 // Shared body of backward and train.  Caller's stream: q build → gather loop →
 // epilogue → entity pass → finalise; side stream: CSR ∥ row pass, relation pass ∥ entity pass.
 int run_grad(const kge_model_desc* m, const Geom& geo, int mode, const int64_t* pos, const int64_t* neg,
@@ -381,6 +402,7 @@ int run_grad(const kge_model_desc* m, const Geom& geo, int mode, const int64_t* 
   ea.dma = (nsl > 0 && (double)B * Le * 4.0 < 2147483648.0 && env_int("KGE_ENT_DMA", 0) != 0) ? 1 : 0;
   ea.adam = adam_t(adam ? &adam->entity : nullptr);
   ea.adamk = ak;
+  ea.align_sl = entity_slice_align(nsl, geo.eg.S, Le, m->entity_embedding, write_grad ? grad_entity : nullptr, ea.adam);
   ea.rel = rl;
   ea.B = B;
   ea.rel_blocks = rel_fused ? (m->nrelation + 3) / 4 : 0;

@@ -137,6 +137,7 @@ struct EntArgs {
   int64_t B;            // batch rows (the q buffer's height)
   int nsl;              // > 0: column-sliced pass k_entity_sl with nsl slices of slice_w slots (VEC = 4)
   int slice_w;
+  int align_sl;         // k_entity_sl: line-aligned 64-slot slices per row (entity_slice_align)
   int dma;              // k_entity_sl stages the q slices by LDS-DMA (needs B·Le·4 < 2^31)
   AdamT adam;           // fused optimizer step (adam.p == null: none)
   AdamK adamk;

@@ -514,7 +514,8 @@ def test_config2_full_size_properties():
 
 @pytest.mark.parametrize("name,d,B", [("RotatE", 200, 24), ("ComplEx", 200, 24), ("TransE", 200, 24),
                                       ("pRotatE", 200, 24), ("DistMult", 200, 24), ("RotatE", 104, 1100),
-                                      ("DistMult", 52, 700)])
+                                      ("DistMult", 52, 700), ("RotatE", 1000, 24), ("DistMult", 1000, 24),
+                                      ("ComplEx", 1000, 24)])
 def test_entity_pass_column_slices_bitwise(name, d, B, monkeypatch):
     """The column-sliced entity pass (k_entity_sl with nsl = 1, 2, 4, 8
     slices — the count is picked per shape — with the q slices loaded into
@@ -522,7 +523,10 @@ def test_entity_pass_column_slices_bitwise(name, d, B, monkeypatch):
     (k_entity, the path for rows that are not float4-aligned; KGE_ENT_SLICES=0
     forces it here) apply the same per-element arithmetic in the same
     occurrence order: identical gradients and fused Adam updates, bit for bit
-    (the regulariser's partial sums only regroup)."""
+    (the regulariser's partial sums only regroup).  d = 1000 (250 slots per
+    (half) row, 4 slices): the line-aligned slices (the default there, rows of
+    16-B phase 0/4 — DistMult 0/2/4/6) against the even split (KGE_ENT_ALIGN=0,
+    suffix "u")."""
     E, R, n = 300, 7, 40   # d = 200: 50 slots per (half) row: 1..8 slices all fit
     args = Namespace(negative_adversarial_sampling=True, adversarial_temperature=1.0, uni_weight=False,
                      regularization=1e-4 if name in ("ComplEx", "DistMult") else 0.0)
@@ -530,10 +534,12 @@ def test_entity_pass_column_slices_bitwise(name, d, B, monkeypatch):
     P, N, W = torch.from_numpy(pos).to(DEV), torch.from_numpy(neg).to(DEV), torch.from_numpy(w).to(DEV)
     out = {}
     # "<slices>d": the same slices with the q slices staged by LDS-DMA (KGE_ENT_DMA=1)
-    variants = ("0", "1", "2", "4", "8", "1d", "4d", "8d") if d == 200 else ("0", "-1", "-1d")
+    variants = {200: ("0", "1", "2", "4", "8", "1d", "4d", "8d"), 1000: ("0", "4", "4u", "4d", "4ud")}.get(
+        d, ("0", "-1", "-1d"))
     for nsl in variants:
-        monkeypatch.setenv("KGE_ENT_SLICES", nsl.rstrip("d"))
-        monkeypatch.setenv("KGE_ENT_DMA", "1" if nsl.endswith("d") else "0")
+        monkeypatch.setenv("KGE_ENT_SLICES", nsl.rstrip("ud"))
+        monkeypatch.setenv("KGE_ENT_DMA", "1" if "d" in nsl else "0")
+        monkeypatch.setenv("KGE_ENT_ALIGN", "0" if "u" in nsl else "1")
         m, *_ = build_model(name, E, R, d, 12.0, 5)
         opt = KGEAdam([p for p in m.parameters() if p.requires_grad], lr=1e-3)
         res = []
