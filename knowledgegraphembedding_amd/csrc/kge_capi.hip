@@ -269,7 +269,10 @@ int run_grad(const kge_model_desc* m, const Geom& geo, int mode, const int64_t* 
   const int write_grad = (!adam || adam->write_grad) ? 1 : 0;
   const Consts c = consts_of(m);
   const int Le = m->entity_dim, Lr = m->relation_dim;
-  const size_t lds = sizeof(float) * (2 * 64 * (size_t)geo.ns * geo.vec + (size_t)vb_floats(Le) + (size_t)ra.n_lds + 32);
+  // k_row's LDS: q (2 padded halves), the merge buffer, the raw scores, the
+  // wave states and, with the fused epilogue, the positive's element terms
+  const size_t lds = sizeof(float) * (2 * 64 * (size_t)geo.ns * geo.vec + (size_t)vb_floats(Le) + (size_t)ra.n_lds + 32 +
+                                      (ra.fuse_epi ? 64 * (size_t)geo.ns * geo.vec : 0));
   if (lds > 64 * 1024) return KGE_ERR_DIM;
   const bool all = (phases == KGE_PHASE_ALL);
   if (e_end < 0) e_end = m->nentity;
