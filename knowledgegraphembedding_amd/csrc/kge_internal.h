@@ -147,6 +147,13 @@ struct EntArgs {
   int fin_fused;        // (only when nothing it reads is written by this launch)
 };
 
+// k_entity_sl's leading blocks: the fused finalisation and the relation rows,
+// rounded up to a multiple of 8 (the XCD count) when there are any
+__host__ __device__ inline unsigned ent_lead_blocks(const EntArgs& a) {
+  const unsigned l = (unsigned)a.rel_blocks + (a.fin_fused ? 1u : 0u);
+  return (l + 7u) & ~7u;
+}
+
 // Near-tie window of the fast ranking passes (all three): a candidate whose
 // fast fp32 score lies within delta[q] of the query's fast true score is not
 // counted but listed for the reference-order refinement (kge_rank_ref.h).
