@@ -3,11 +3,13 @@ cd "${GRAFT_REPO_ROOT}"
 mkdir -p gpurun_out/warm
 cd /tmp && export TMPDIR=/tmp
 R=$GRAFT_REPO_ROOT
-for v in A B C; do
+for v in ${VARIANTS:-A B C}; do
   case $v in
-    A) E="KGE_X=0"; X="";;
-    B) E="KGE_DBG_NOSYNC_WARMUP=1"; X="";;
-    C) E="KGE_X=0"; X="--no-stage-timer";;
+    A) E="KGE_X=0"; X="--no-rank";;
+    B) E="KGE_DBG_NOSYNC_WARMUP=1"; X="--no-rank";;
+    C) E="KGE_X=0"; X="--no-stage-timer --no-rank";;
+    D) E="KGE_BENCH_RANK_FIRST=1"; X="";;
+    E) E="KGE_DBG_PRESTEPS=100"; X="--no-rank";;
   esac
-  env $E timeout -k 10 200 rocprofv3 --kernel-trace --output-format csv -d $R/gpurun_out/warm/$v -o run -- python3 $R/bench.py --steps 60 --warmup 5 --no-cpu-baseline --no-rank $X > $R/gpurun_out/warm/$v.json 2> $R/gpurun_out/warm/$v.err || exit $?
+  env $E timeout -k 10 200 rocprofv3 --kernel-trace --output-format csv -d $R/gpurun_out/warm/$v -o run -- python3 $R/bench.py --steps 60 --warmup 5 --no-cpu-baseline $X > $R/gpurun_out/warm/$v.json 2> $R/gpurun_out/warm/$v.err || exit $?
 done
