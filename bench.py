@@ -335,16 +335,9 @@ def main():
     else:
         it = DeviceBatches(dev, seed=1000 + rank)
 
-    rank_first = os.environ.get("KGE_BENCH_RANK_FIRST", "0") == "1"
-    ranking = None
-    if rank_first and rank == 0 and world == 1 and not a.no_rank and a.workload == "fb15k":
-        ranking = rank_section(dev)
-    for _ in range(int(os.environ.get("KGE_DBG_PRESTEPS", "0"))):  # diagnostic: settled-state timing
-        KGEModel.train_step(model, opt, it, args)
     for _ in range(a.warmup):
         KGEModel.train_step(model, opt, it, args)
-    if os.environ.get("KGE_DBG_NOSYNC_WARMUP", "0") != "1":  # diagnostic (the contract syncs here)
-        torch.cuda.synchronize()
+    torch.cuda.synchronize()
 
     lib = _lib.load()
     # per-stage HIP events on one step in TIMER_PERIOD (every step's events cost ~4 %)
@@ -458,9 +451,7 @@ def main():
     fr = [x for x in fr if x is not None]
     if any(f > 1.0 for f in fr):
         print(f"bench.py: a roofline fraction exceeds 1 ({fr}); the byte model is wrong", file=sys.stderr)
-    if ranking is not None:
-        out["ranking"] = ranking
-    elif rank == 0 and world == 1 and not a.no_rank and a.workload == "fb15k":
+    if rank == 0 and world == 1 and not a.no_rank and a.workload == "fb15k":
         out["ranking"] = rank_section(dev)
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(cpu_state, budget_s=a.cpu_budget)

@@ -1,4 +1,9 @@
 #!/bin/bash
+# Per-step kernel durations of the first 65 training steps under rocprofv3
+# (profiles/r03/warm/).  Variants B (no synchronize after the warmup), D (the
+# ranking section before the warmup) and E (100 extra training steps first)
+# used temporary diagnostic switches of bench.py that were removed after the
+# measurement; A and C run on the current bench.py.
 cd "${GRAFT_REPO_ROOT}"
 mkdir -p gpurun_out/warm
 cd /tmp && export TMPDIR=/tmp
