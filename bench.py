@@ -432,7 +432,7 @@ def main():
                      "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS if achieved else None,
                      "traffic": row_traffic, "algorithmic_bytes_per_launch": row_bytes,
                      "avg_launch_ms": row_ms, "pattern_ceiling": ceiling},
-        "roofline_entity": {"bound": "hbm", "kernel": "k_entity_sl (entity-major gradient + fused Adam; relation rows in trailing blocks)",
+        "roofline_entity": {"bound": "hbm", "kernel": "k_entity_sl (entity-major gradient + fused Adam; loss finalisation and relation rows in leading blocks)",
                             "achieved": ent_achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                             "frac": ent_achieved / HBM_PEAK_GBS if ent_achieved else None, "traffic": ent_traffic,
                             "algorithmic_bytes_per_launch": ent_bytes, "avg_launch_ms": ent_ms,
