@@ -76,6 +76,8 @@ struct RowArgs {
   int32_t* err;
   void (*timer_mid)(hipStream_t);  // stage-timer hook between the row-pass launches (or null)
   ShipArgs sh;        // query shipping stages only
+  float* q_sl;        // non-null (VEC = 4): q also slice-major for k_entity_sl, [slice][row][re 64 | im 64 slots]
+  int q_sl_w;         //   slots per slice
 };
 
 // k_row's LDS merge buffer: [2][Le] floats, and at least the 256 floats the
@@ -138,6 +140,7 @@ struct EntArgs {
   int nsl;              // > 0: column-sliced pass k_entity_sl with nsl slices of slice_w slots (VEC = 4)
   int slice_w;
   int align_sl;         // k_entity_sl: line-aligned 64-slot slices per row (entity_slice_align)
+  const float* q_sl;    // k_entity_sl<.., QSL>: q slice-major (written by k_row; even slices only) or null
   int dma;              // k_entity_sl stages the q slices by LDS-DMA (needs B·Le·4 < 2^31)
   AdamT adam;           // fused optimizer step (adam.p == null: none)
   AdamK adamk;

@@ -534,12 +534,13 @@ def test_entity_pass_column_slices_bitwise(name, d, B, monkeypatch):
     P, N, W = torch.from_numpy(pos).to(DEV), torch.from_numpy(neg).to(DEV), torch.from_numpy(w).to(DEV)
     out = {}
     # "<slices>d": the same slices with the q slices staged by LDS-DMA (KGE_ENT_DMA=1)
-    variants = {200: ("0", "1", "2", "4", "8", "1d", "4d", "8d"), 1000: ("0", "4", "4u", "4d", "4ud")}.get(
-        d, ("0", "-1", "-1d"))
+    variants = {200: ("0", "1", "2", "4", "8", "1d", "4d", "8d", "4q"), 1000: ("0", "4", "4u", "4d", "4ud", "4q")}.get(
+        d, ("0", "-1", "-1d", "-1q"))
     for nsl in variants:
-        monkeypatch.setenv("KGE_ENT_SLICES", nsl.rstrip("ud"))
+        monkeypatch.setenv("KGE_ENT_SLICES", nsl.rstrip("udq"))
         monkeypatch.setenv("KGE_ENT_DMA", "1" if "d" in nsl else "0")
         monkeypatch.setenv("KGE_ENT_ALIGN", "0" if "u" in nsl else "1")
+        monkeypatch.setenv("KGE_ENT_QSL", "1" if "q" in nsl else "0")
         m, *_ = build_model(name, E, R, d, 12.0, 5)
         opt = KGEAdam([p for p in m.parameters() if p.requires_grad], lr=1e-3)
         res = []
