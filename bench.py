@@ -170,27 +170,28 @@ def host_cores() -> int:
     return n
 
 
-def cpu_baseline(model_cpu_state, budget_s: float = 12.0, b: int = 32):
-    """The oracle (reference op chain on CPU fp32, + torch.optim.Adam) on a
-    bounded sample of the same workload: b positives x 256 negatives, on every
-    host core this process may run on.  The per-triple rate grows a little
-    with b: measured in the build container on 8 cores, b = 32 gives 3.9 k and
-    b = 1024 5.0 k triples/s (profiles/r02/cpu_baseline_bscaling.json), so the
-    bounded b = 32 sample understates the full-batch CPU rate by about 1.26x;
-    the line carries that ratio next to the sample."""
+def cpu_baseline(model_cpu_state, budget_s: float = 30.0, b: int = B, max_steps: int = 2):
+    """The oracle (the reference's ATen op chain on CPU fp32 + torch.optim.Adam)
+    on the workload itself — BASELINE config 2's full b = 1024 × n = 256 step
+     — on every host core this process may run on: one small
+    warm-up step (b = 16: thread pool and allocator), then full-batch steps,
+    tail- then head-batch, until `max_steps` are timed or `budget_s` has
+    passed after the first (a full step takes ≈ 20-40 s on 8-16 cores)."""
     from oracle import kge_oracle as O
     ent, rel, erange = model_cpu_state
     cores = host_cores()
     torch.set_num_threads(cores)
     g = torch.Generator().manual_seed(7)
-    pos = torch.stack([torch.randint(0, E, (b,), generator=g), torch.randint(0, R, (b,), generator=g),
-                       torch.randint(0, E, (b,), generator=g)], 1)
-    neg = torch.randint(0, E, (b, NNEG), generator=g)
-    w = torch.rand(b, generator=g) * 0.3 + 0.1
+
+    def batch(nb):
+        pos = torch.stack([torch.randint(0, E, (nb,), generator=g), torch.randint(0, R, (nb,), generator=g),
+                           torch.randint(0, E, (nb,), generator=g)], 1)
+        return pos, torch.randint(0, E, (nb, NNEG), generator=g), torch.rand(nb, generator=g) * 0.3 + 0.1
+
     params = [ent.clone().requires_grad_(True), rel.clone().requires_grad_(True)]
     opt = torch.optim.Adam(params, lr=1e-4)
 
-    def step(mode):
+    def step(mode, pos, neg, w):
         _, ge, gr, _ = O.train_grads("RotatE", params[0].detach(), params[1].detach(), None, pos, neg, w, mode,
                                      adversarial=True, temperature=TEMP, uni_weight=False, regularization=0.0,
                                      gamma=GAMMA, erange=erange)
@@ -198,21 +199,19 @@ def cpu_baseline(model_cpu_state, budget_s: float = 12.0, b: int = 32):
         params[0].grad, params[1].grad = ge, gr
         opt.step()
 
-    step('tail-batch')  # warm-up
-    t0 = time.perf_counter()
-    k = 0
-    while True:
-        step('head-batch' if k % 2 else 'tail-batch')
-        k += 1
-        if time.perf_counter() - t0 > budget_s or k >= 16:
-            break
-    dt = time.perf_counter() - t0
-    return {"value": k * b * (NNEG + 1) / dt, "unit": "triples/s", "cores": cores, "cpu_model": _cpu_model(),
-            "kind": "port", "b1024_over_b32_rate": 1.264,
-            "b_scaling_source": "profiles/r02/cpu_baseline_bscaling.json (build container, 8 cores)",
-            "sample": f"oracle train step (ATen op chain fwd + autograd bwd + torch Adam), RotatE E={E} R={R} "
-                      f"d={D} b={b} n={NNEG} adv, {k} timed steps after 1 warm-up, {dt:.1f} s, "
-                      f"torch threads = {cores}"}
+    step('tail-batch', *batch(16))  # warm-up
+    full = batch(b)
+    times = []
+    while len(times) < max_steps and (not times or sum(times) < budget_s):
+        t0 = time.perf_counter()
+        step('head-batch' if len(times) % 2 else 'tail-batch', *full)
+        times.append(time.perf_counter() - t0)
+    dt = sum(times)
+    return {"value": len(times) * b * (NNEG + 1) / dt, "unit": "triples/s", "cores": cores,
+            "cpu_model": _cpu_model(), "kind": "port", "step_s": [round(x, 2) for x in times],
+            "sample": f"oracle train step (ATen op chain fwd + autograd bwd + torch Adam), the workload's own "
+                      f"RotatE E={E} R={R} d={D} b={b} n={NNEG} adv; {len(times)} timed full-batch steps "
+                      f"(tail, head) after a b=16 warm-up, {dt:.1f} s, torch threads = {cores}"}
 
 
 def rank_section(dev, reps: int = 3) -> dict:
@@ -221,12 +220,12 @@ def rank_section(dev, reps: int = 3) -> dict:
     tile + near-tie refinement in the reference's order) of all 3134
     wn18rr-shape test triples in both directions (6268 queries, E=40943, d=500)
     against a synthetic filter graph of wn18rr's 93,003 true triples
-    (tools/bench_rank.py, same data).  `tflops` = 2·queries·E·K / wall time of
-    the whole pass (host CSR, bitmap, operand split, window, MFMA tile,
-    refinement, read-back) in fp32-product terms; the tile computes each fp32
-    product as four bf16 MFMA products (x = x_hi + x_lo), so `frac` against
-    the fp32 MFMA peak can pass 1 and `bf16_frac` = 4·flops / time / 2.5 PF is
-    the matrix cores' own share (tile alone: profiles/r03/rank/)."""
+    (tools/bench_rank.py, same data).  The tile computes each fp32 product as
+    four bf16 MFMA products (x = x_hi + x_lo): `frac` = the bf16 flops the
+    matrix cores issue (tile padding included) / wall time of the whole pass
+    (host CSR, bitmap, operand split, window, MFMA tile, refinement,
+    read-back) / the 2.5 PF bf16 dense spec; `fp32_equivalent_tflops` =
+    2·queries·E·K / the same time (tile alone: profiles/r0x/rank/)."""
     import numpy as np
     from knowledgegraphembedding_amd import synth
     from knowledgegraphembedding_amd.filters import FilterIndex
@@ -250,10 +249,17 @@ def rank_section(dev, reps: int = 3) -> dict:
             dt = time.perf_counter() - t0
             if rep and (best is None or dt < best):
                 best = dt
-        flops = 2.0 * 2 * ntest * Ew * K
-        out[name] = {"ms": best * 1e3, "queries_per_s": 2 * ntest / best, "tflops": flops / best / 1e12,
-                     "fp32_mfma_peak_tflops": 157.3, "frac": flops / best / 1e12 / 157.3,
-                     "bf16_frac": 4 * flops / best / 1e12 / 2500.0,
+        flops = 2.0 * 2 * ntest * Ew * K  # fp32 products the ranking needs (both directions)
+        # what the matrix cores issue: four bf16 products per fp32 product over
+        # the tile-padded shape (128-query and 128-candidate tiles, 16-k slabs)
+        pad = lambda x, m: -(-x // m) * m  # noqa: E731
+        issued = 2.0 * 4 * 2 * pad(ntest, 128) * pad(Ew, 128) * pad(K, 16)
+        out[name] = {"ms": best * 1e3, "queries_per_s": 2 * ntest / best,
+                     "bf16_issued_tflops": issued / best / 1e12, "peak_tflops": 2500.0,
+                     "frac": issued / best / 1e12 / 2500.0,
+                     "fp32_equivalent_tflops": flops / best / 1e12,
+                     "what": "whole pass wall time (host filter CSR, bitmap, operand split, window, MFMA tile, "
+                             "refinement, read-back); frac = issued bf16 MFMA flops / 2.5 PF bf16 dense spec",
                      "path": "split-bf16 MFMA tile (4 bf16 products per fp32 product) + reference-order refinement",
                      "mrr": float(np.mean(1.0 / np.concatenate([rh, rt])))}
         del m
@@ -267,7 +273,7 @@ def main():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-budget", type=float, default=12.0)
+    ap.add_argument("--cpu-budget", type=float, default=30.0)
     ap.add_argument("--no-stage-timer", action="store_true",
                     help="skip the per-stage HIP events (roofline then comes from the committed rocprof summary)")
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="fb15k")
@@ -379,13 +385,16 @@ def main():
     achieved = row_bytes / (row_ms * 1e-3) / 1e9 if row_ms > 0 else None
     ent_achieved = ent_bytes / (ent_ms * 1e-3) / 1e9 if ent_ms > 0 else None
     row_traffic = ent_traffic = None
-    if a.workload == "fb15k" and not exchanged:  # PMC summaries of this workload (tools/profile.sh + tools/pmc_traffic.py)
+    # the committed PMC summaries and pattern ceilings were measured on the
+    # workload's own shape (d = 1000): not applicable to a --hidden-dim run
+    own_shape = not a.hidden_dim or a.hidden_dim == wl["D"]
+    if a.workload == "fb15k" and not exchanged and own_shape:  # PMC summaries of this workload (tools/profile.sh + tools/pmc_traffic.py)
         row_traffic = _pmc_bytes(a.traffic_json or os.path.join(here, "profiles", "pmc_traffic.json"))
         ent_traffic = _pmc_bytes(os.path.join(here, "profiles", "pmc_traffic_entity.json"))
 
     ceiling = None  # k_row's access pattern alone (tools/dbg/gather_ceiling.hip), measured on MI355X
     cj = os.path.join(here, "profiles", "r01", "gather_ceiling.jsonl")
-    if a.workload == "fb15k" and os.path.exists(cj) and achieved:
+    if a.workload == "fb15k" and own_shape and os.path.exists(cj) and achieved:
         with open(cj) as f:
             c0 = json.loads(f.readline())
         ceiling = {"GBps": c0["GBps"], "frac": achieved / c0["GBps"], "source": "profiles/r01/gather_ceiling.jsonl",
@@ -393,7 +402,7 @@ def main():
 
     ent_ceiling = None  # the entity pass's HBM stream alone (tools/dbg/stream_ceiling.hip), measured on MI355X
     sj = os.path.join(here, "profiles", "entity_stream_ceiling.jsonl")
-    if a.workload == "fb15k" and os.path.exists(sj) and ent_achieved:
+    if a.workload == "fb15k" and own_shape and os.path.exists(sj) and ent_achieved:
         with open(sj) as f:
             best = max((json.loads(line) for line in f if line.strip()), key=lambda r: r["GBps"])
         ent_ceiling = {"GBps": best["GBps"], "frac": ent_achieved / best["GBps"],
@@ -402,6 +411,16 @@ def main():
                                "non-temporal), without the entity pass's 2.1 GB of q-slice gathers from L2"}
 
     value = a.steps * B * (NNEG + 1) * world / dt
+    # what the process group itself saw (the driver's multi-GPU record can
+    # check that RCCL ran over N ranks): backend, its world size, RCCL version
+    dist_info = {"backend": None, "world_size": 1, "rccl_version": None}
+    if group is not None:
+        dist_info["backend"] = str(dist.get_backend(group))
+        dist_info["world_size"] = dist.get_world_size(group)
+    try:
+        dist_info["rccl_version"] = ".".join(str(x) for x in torch.cuda.nccl.version())
+    except Exception:  # noqa: BLE001 — reported as unknown, never fatal
+        pass
     out = {
         "metric": METRIC,
         "value": value,
@@ -422,6 +441,7 @@ def main():
                    "entities": E, "relations": R, "hidden_dim": D, "batch_per_gpu": B, "global_batch": B * world,
                    "negatives": NNEG, "adversarial_temperature": TEMP, "gamma": GAMMA,
                    "parallelism": (f"rowpart{world}" if wl["partition"] and part is not None else f"dp{world}")},
+        "dist": dist_info,
         "stage_timed_steps": int(stage[6]),
         # HIP-event stage times of one step in TIMER_PERIOD, on the launching
         # stream; the CSR runs on a side stream beside the row pass, so these
@@ -454,7 +474,9 @@ def main():
     if rank == 0 and world == 1 and not a.no_rank and a.workload == "fb15k":
         out["ranking"] = rank_section(dev)
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(cpu_state, budget_s=a.cpu_budget)
+        # the full batch at config 2's n = 256; config 5's n = 1024 at a quarter of the rows (one full
+        # step there would hold ~40 GB of temporaries and take minutes)
+        out["cpu_baseline"] = cpu_baseline(cpu_state, budget_s=a.cpu_budget, b=B if NNEG <= 256 else B // 4)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if group is not None:

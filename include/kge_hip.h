@@ -55,12 +55,14 @@ enum kge_status {
     KGE_ERR_ARG = 4,        /* null pointer / negative size */
     KGE_ERR_WORKSPACE = 5,  /* workspace smaller than *_workspace_bytes() */
     KGE_ERR_DIM = 6,        /* row length beyond what the kernels are instantiated for */
+    KGE_ERR_ABI = 7,        /* kge_model_desc.struct_size != sizeof(kge_model_desc) of this library */
     KGE_ERR_HIP_BASE = 1000 /* + hipError_t */
 };
 
 /* Device-side error bits written to *err_flag. */
 #define KGE_DEVERR_INDEX 1
 #define KGE_DEVERR_SAMPLER 2 /* a row's true list left no room within max_draws draws */
+#define KGE_DEVERR_ARG 4     /* kge_rank_sin_args: item_off does not match the listed counts */
 
 /*
  * The parameters of one KGEModel (model.py:22-70).
@@ -80,7 +82,7 @@ typedef struct kge_model_desc {
     int32_t model;
     int32_t entity_dim;   /* floats per entity row   (model.py:42) */
     int32_t relation_dim; /* floats per relation row (model.py:43) */
-    int32_t reserved;
+    int32_t struct_size;  /* = sizeof(kge_model_desc) as the caller compiled it (else KGE_ERR_ABI) */
     int64_t nentity;
     int64_t nrelation;
     float gamma;          /* model.py:32-35 */
@@ -93,7 +95,10 @@ typedef struct kge_model_desc {
     const float *relation_trig;      /* RotatE [nrelation, 2, relation_dim] or NULL (ranking only) */
 } kge_model_desc;
 
-/* Library identity (for the loader's symbol check). */
+/* Library identity: "knowledgegraphembedding_amd <KGE_ABI_VERSION> gfx950".  The
+ * version changes with every change of a struct or signature in this header;
+ * loaders refuse a library whose version differs from the header they bind. */
+#define KGE_ABI_VERSION "0.2"
 const char *kge_version(void);
 const char *kge_status_string(int status);
 
@@ -399,7 +404,9 @@ int kge_adam_step(float *param, const float *grad, float *exp_avg, float *exp_av
  * (without it: correctly rounded values, which differ from the reference's
  * CPU vector library in the last bit on a few percent of arguments).
  * pRotatE's sin acts on per-candidate phase sums, so it cannot be tabulated:
- * correctly rounded there (ranks equal the reference's up to that last bit).
+ * correctly rounded in this one-call form (ranks equal the reference's up to
+ * that last bit); bit-exact with the three-call form below
+ * (KGE_RANK_STAGE_LIST, kge_rank_sin_args, kge_rank_finish_sin).
  */
 size_t kge_rank_workspace_bytes(const kge_model_desc *m, int64_t nq);
 int kge_rank_filtered(const kge_model_desc *m, int32_t mode, const int64_t *queries, int64_t nq,
@@ -414,17 +421,54 @@ int kge_rank_filtered(const kge_model_desc *m, int32_t mode, const int64_t *quer
  * listed_out [nq] int32 (nullable): near-ties re-scored per query (above the
  * 1024-per-query list capacity the query is rescanned exactly).  Every path
  * returns the same ranks and ties.  path | KGE_RANK_REUSE_TABLE: the caller
- * asserts that an earlier call on this same workspace (same pointer, not
- * written in between, stream-ordered before this one) ranked with the same
- * model and an unchanged entity table — the other direction or another query
- * block of one evaluation, any nq — so the table's statistics and split
- * operands it left at the start of the workspace are reused.
+ * asserts that the entity table's CONTENTS are unchanged since the last
+ * ranking call on this workspace (the other direction or another query block
+ * of one evaluation, any nq).  The table statistics and split operands that
+ * call left at the start of the workspace are reused only where a tag written
+ * beside them (on the device, stream-ordered) shows they were written for the
+ * same table pointer and shape — a call on another table, or one whose path
+ * wrote no split operands, makes this call recompute them.
  */
 #define KGE_RANK_REUSE_TABLE 0x100
+/* path | KGE_RANK_STAGE_LIST (pRotatE only, listed_out required, ranks_out
+ * unused): stop after the fast pass — listed_out holds each query's near-tie
+ * count and the lists stay in the workspace for kge_rank_sin_args /
+ * kge_rank_finish_sin below. */
+#define KGE_RANK_STAGE_LIST 0x200
+#define KGE_RANK_LIST_CAP 1024 /* listed near-ties per query; above it the query is rescanned in full */
 int kge_rank_filtered_ex(const kge_model_desc *m, int32_t mode, const int64_t *queries, int64_t nq,
                          const int64_t *filt_off, const int64_t *filt_ids, int64_t *ranks_out,
                          int32_t *ties_out, int32_t *listed_out, int32_t path, void *workspace,
                          size_t workspace_bytes, int32_t *err_flag, void *stream);
+
+/*
+ * pRotatE ranks bit-exact to the reference — whose sin (model.py:245) is its
+ * CPU vector library's (ATen → MKL VML here), which no device instruction
+ * sequence reproduces — in three calls on one stream and workspace:
+ *   1. kge_rank_filtered_ex(..., path | KGE_RANK_STAGE_LIST, listed_out): fast
+ *      pass, windows widened by the library's ≤ 1 ulp, near-tie lists.
+ *   2. the caller reads listed_out and sets item_off [nq + 1] (device int64,
+ *      exclusive scan) to n_items(q) = 1 + listed_out[q], or 1 + nentity when
+ *      listed_out[q] > KGE_RANK_LIST_CAP (every candidate is rescanned);
+ *      kge_rank_sin_args writes args_out [item_off[nq], entity_dim]: per item
+ *      (0 = the true entity, then the listed candidates / entity ids in order)
+ *      the K phase sums θh + (θr − θt) (head-batch) or (θh + θr) − θt
+ *      (tail-batch) the reference takes the sin of (model.py:236-245; IEEE
+ *      divisions and adds, host-independent).  A query whose range does not
+ *      match its count is skipped and sets KGE_DEVERR_ARG.
+ *   3. the caller evaluates sin_values = sin(args) with the reference's own
+ *      library call (torch.sin on the host CPU) and kge_rank_finish_sin
+ *      re-scores every item from those values in the reference's order
+ *      (abs, ATen sum(dim=2), × modulus, γ −) and writes ranks / ties / listed
+ *      as kge_rank_filtered_ex does.
+ * The queries, filters and mode of step 1 stay in the workspace; steps 2-3
+ * pass the same mode, nq and workspace.
+ */
+int kge_rank_sin_args(const kge_model_desc *m, int32_t mode, int64_t nq, const int64_t *item_off, float *args_out,
+                      void *workspace, size_t workspace_bytes, int32_t *err_flag, void *stream);
+int kge_rank_finish_sin(const kge_model_desc *m, int32_t mode, int64_t nq, const int64_t *item_off,
+                        const float *sin_values, int64_t *ranks_out, int32_t *ties_out, int32_t *listed_out,
+                        void *workspace, size_t workspace_bytes, int32_t *err_flag, void *stream);
 
 /*
  * Live stage timing for benchmarks (no reference counterpart): when enabled,

@@ -17,19 +17,27 @@ MODEL_IDS = {"TransE": 0, "DistMult": 1, "ComplEx": 2, "RotatE": 3, "pRotatE": 4
 MODE_IDS = {"single": 0, "head-batch": 1, "tail-batch": 2}
 DEVERR_INDEX = 1
 DEVERR_SAMPLER = 2
+DEVERR_ARG = 4
+ABI_VERSION = "0.2"  # KGE_ABI_VERSION of the include/kge_hip.h this binding mirrors
+RANK_STAGE_LIST = 0x200  # KGE_RANK_STAGE_LIST
+RANK_LIST_CAP = 1024  # KGE_RANK_LIST_CAP
 PHASE_ROWS, PHASE_ENTITY, PHASE_FINALIZE, PHASE_ALL = 1, 2, 4, 7
 SHIP_Q, SHIP_ROWS, SHIP_MERGE, SHIP_CHAIN, SHIP_ENTITY = 1, 2, 3, 4, 5
 ERR_HIP_BASE = 1000
 
 
 class ModelDesc(C.Structure):
-    """struct kge_model_desc."""
+    """struct kge_model_desc (struct_size is set on construction)."""
+
+    def __init__(self, *a, **k):
+        super().__init__(*a, **k)
+        self.struct_size = C.sizeof(ModelDesc)
 
     _fields_ = [
         ("model", C.c_int32),
         ("entity_dim", C.c_int32),
         ("relation_dim", C.c_int32),
-        ("reserved", C.c_int32),
+        ("struct_size", C.c_int32),
         ("nentity", C.c_int64),
         ("nrelation", C.c_int64),
         ("gamma", C.c_float),
@@ -133,6 +141,8 @@ SIGNATURES = {
     "kge_rank_workspace_bytes": (_SZ, [_DESC, _I64]),
     "kge_rank_filtered": (C.c_int, [_DESC, _I32, _P, _I64, _P, _P, _P, _P, _P, _SZ, _P, _P]),
     "kge_rank_filtered_ex": (C.c_int, [_DESC, _I32, _P, _I64, _P, _P, _P, _P, _P, _I32, _P, _SZ, _P, _P]),
+    "kge_rank_sin_args": (C.c_int, [_DESC, _I32, _I64, _P, _P, _P, _SZ, _P, _P]),
+    "kge_rank_finish_sin": (C.c_int, [_DESC, _I32, _I64, _P, _P, _P, _P, _P, _P, _SZ, _P, _P]),
     "kge_stage_timer": (C.c_int, [_I32, _P, _I32]),
     "kge_sample_negatives": (C.c_int, [_P, _I64, _P, _I64, _I64, _I64, _P, _P, _P, _P, C.c_uint64, _I64, _P, _P, _P,
                                        _P, _P]),
@@ -160,6 +170,10 @@ def load() -> C.CDLL:
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
+    version = lib.kge_version().decode()
+    if version.split()[1:2] != [ABI_VERSION]:
+        raise KGEHipError(f"{LIB_PATH} reports ABI {version!r}; this binding mirrors kge_hip.h ABI {ABI_VERSION}: "
+                          "rebuild the library (python -m knowledgegraphembedding_amd.build)")
     _lib = lib
     return lib
 

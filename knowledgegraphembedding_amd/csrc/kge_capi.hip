@@ -31,6 +31,8 @@ bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
 // model.py:63-70 plus the broadcast rules of the plug-ins.
 int check_model(const kge_model_desc* m, Geom* g) {
   if (!m) return KGE_ERR_ARG;
+  // a caller built against another layout of this struct (KGE_ABI_VERSION)
+  if (m->struct_size != (int32_t)sizeof(kge_model_desc)) return KGE_ERR_ABI;
   if (m->model < KGE_TRANSE || m->model > KGE_PROTATE) return KGE_ERR_MODEL;
   if (!m->entity_embedding || !m->relation_embedding) return KGE_ERR_ARG;
   if (m->nentity <= 0 || m->nrelation <= 0 || m->entity_dim <= 0 || m->relation_dim <= 0) return KGE_ERR_ARG;
@@ -84,7 +86,7 @@ int rank_path(const kge_model_desc* m, int requested) {
   if (requested == RP_SCAN) return RP_SCAN;
   return x_ok ? RP_MFMA : mfma_ok ? RP_MFMA32 : (tile_ok ? RP_TILE : RP_SCAN);
 }
-constexpr int RANK_CAP = 1024;  // listed near-ties per query before the exact rescan takes over
+constexpr int RANK_CAP = KGE_RANK_LIST_CAP;  // listed near-ties per query before the exact rescan takes over
 
 Consts consts_of(const kge_model_desc* m) {
   Consts c;
@@ -473,7 +475,7 @@ using namespace kge;
 
 extern "C" {
 
-const char* kge_version(void) { return "knowledgegraphembedding_amd 0.1 gfx950"; }
+const char* kge_version(void) { return "knowledgegraphembedding_amd " KGE_ABI_VERSION " gfx950"; }
 
 const char* kge_status_string(int status) {
   switch (status) {
@@ -484,6 +486,7 @@ const char* kge_status_string(int status) {
     case KGE_ERR_ARG: return "invalid argument";
     case KGE_ERR_WORKSPACE: return "workspace too small";
     case KGE_ERR_DIM: return "row length / negative count outside the compiled kernel range";
+    case KGE_ERR_ABI: return "kge_model_desc.struct_size does not match this library (built against another kge_hip.h)";
     default:
       if (status >= KGE_ERR_HIP_BASE) return hipGetErrorString((hipError_t)(status - KGE_ERR_HIP_BASE));
       return "unknown";
@@ -922,6 +925,7 @@ int kge_adam_step(float* param, const float* grad, float* exp_avg, float* exp_av
 namespace kge {
 namespace {
 struct RankWs {
+  int64_t* tag;  // [8] what the table buffers below hold (k_rank_tag)
   float *q, *qref, *s_true, *sref_true, *delta, *stats;
   int64_t* true_id;
   int32_t *gt, *eq, *gtx, *eqx, *ucnt, *ulist;
@@ -933,6 +937,7 @@ RankWs carve_rank(void* ws, const kge_model_desc* m, int64_t nq, size_t* bytes) 
   RankWs w;
   // the entity table's own buffers first, at offsets independent of nq, so a
   // later call on the same workspace can reuse them (KGE_RANK_REUSE_TABLE)
+  w.tag = c.take<int64_t>(8);
   w.stats = c.take<float>(2 + 2 * TS_BLOCKS);  // [max ‖e‖, max |x|, per-block partials]
   // split-bf16 operands: only where the split tile can run (rank_path's x_ok)
   const bool xs = rank_path(m, RP_MFMA) == RP_MFMA;
@@ -965,19 +970,38 @@ size_t kge_rank_workspace_bytes(const kge_model_desc* m, int64_t nq) {
   return b;
 }
 
-int kge_rank_filtered_ex(const kge_model_desc* m, int32_t mode, const int64_t* queries, int64_t nq,
-                         const int64_t* filt_off, const int64_t* filt_ids, int64_t* ranks_out, int32_t* ties_out,
-                         int32_t* listed_out, int32_t path, void* workspace, size_t workspace_bytes,
-                         int32_t* err_flag, void* stream) {
+}  // extern "C"
+
+namespace kge {
+namespace {
+// Stages of one filtered-ranking call (kge_rank_filtered_ex, and pRotatE's
+// three-call form with the caller's sin): RS_LIST runs everything up to the
+// fast pass's near-tie lists and writes only listed_out; RS_ARGS writes the
+// pRotatE phase sums of the listed items; RS_FINISH refines them with the
+// caller's sin values, rescans overflowed windows and writes the ranks.
+enum { RS_ALL = 0, RS_LIST = 1, RS_ARGS = 2, RS_FINISH = 3 };
+
+int rank_impl(const kge_model_desc* m, int32_t mode, const int64_t* queries, int64_t nq, const int64_t* filt_off,
+              const int64_t* filt_ids, int64_t* ranks_out, int32_t* ties_out, int32_t* listed_out, int32_t path,
+              void* workspace, size_t workspace_bytes, int32_t* err_flag, void* stream, int stage,
+              const int64_t* item_off, const float* sins, float* args) {
   Geom geo;
   int st = check_model(m, &geo);
   if (st) return st;
   if (mode != KGE_HEAD_BATCH && mode != KGE_TAIL_BATCH) return KGE_ERR_MODE;
-  if (!queries || !filt_off || !ranks_out || !err_flag || nq < 0) return KGE_ERR_ARG;
+  if (!err_flag || nq < 0) return KGE_ERR_ARG;
+  if (stage == RS_ALL || stage == RS_LIST) {
+    if (!queries || !filt_off) return KGE_ERR_ARG;
+  }
+  if ((stage == RS_ALL || stage == RS_FINISH) && !ranks_out) return KGE_ERR_ARG;
+  if (stage == RS_LIST && !listed_out) return KGE_ERR_ARG;
+  if (stage == RS_ARGS && (!item_off || !args)) return KGE_ERR_ARG;
+  if (stage == RS_FINISH && (!item_off || !sins)) return KGE_ERR_ARG;
+  if (stage != RS_ALL && m->model != KGE_PROTATE) return KGE_ERR_MODEL;
   // KGE_RANK_REUSE_TABLE: the workspace already holds this entity table's
   // statistics and split operands from the previous call (the other direction)
   const bool reuse = (path & KGE_RANK_REUSE_TABLE) != 0;
-  path &= ~KGE_RANK_REUSE_TABLE;
+  path &= ~(KGE_RANK_REUSE_TABLE | KGE_RANK_STAGE_LIST);
   if (path < RP_AUTO || path > RP_MFMA32) return KGE_ERR_ARG;
   if (nq == 0) return KGE_OK;
   if (nq > 65535) return KGE_ERR_DIM;  // the bitmap launch puts queries on grid.y
@@ -1010,36 +1034,9 @@ int kge_rank_filtered_ex(const kge_model_desc* m, int32_t mode, const int64_t* q
   a.prep_only = 1;
   a.zero_counts = 1;
   a.trig = trig;
-  st = launch_status(ops.rank(mode, geo.vec, geo.ns, a, s));
-  if (st) return st;
-  // 2. excluded candidates (filtered ids + the true id) as a bitmap
-  st = launch_status(launch_filter_bits(filt_off, filt_ids, w.true_id, nq, m->nentity, w.bits, err_flag, s));
-  if (st) return st;
-  if (m->model == KGE_DISTMULT || m->model == KGE_COMPLEX || m->model == KGE_PROTATE) {
-    if (!reuse) st = launch_status(launch_table_stats(m->entity_embedding, m->nentity, m->entity_dim, w.stats, s));
-    if (st) return st;
-  }
-  // 3. the fast pass's own s_true (same instruction sequence as its candidates)
-  TileArgs ta;
-  ta.q = w.q; ta.ent = m->entity_embedding; ta.modulus = m->modulus;
-  ta.nq = nq; ta.E = m->nentity; ta.Le = m->entity_dim; ta.K = K;
-  ta.c = a.c; ta.true_id = w.true_id; ta.s_true = w.s_true;
-  ta.fbits = w.bits; ta.W = a.W; ta.gt = w.gt; ta.win = win;
-  if (rp == RP_MFMA) {
-    st = launch_status(launch_split_bf16(w.q, nq, m->entity_dim, w.qs, s));
-    if (!st && !reuse)
-      st = launch_status(launch_split_bf16(m->entity_embedding, m->nentity, m->entity_dim, w.es, s));
-    if (!st)
-      st = launch_status(launch_rank_mfma_x(1, w.qs, w.es, nq, m->nentity, m->entity_dim, w.true_id, w.s_true,
-                                            w.bits, w.gt, win, s));
-  } else if (rp == RP_MFMA32)
-    st = launch_status(launch_rank_mfma(1, w.q, m->entity_embedding, nq, m->nentity, m->entity_dim, w.true_id,
-                                        w.s_true, w.bits, w.gt, win, s));
-  else if (rp == RP_TILE)
-    st = launch_status(ops.rank_tile(mode, 1, ta, s));
-  if (st) return st;
-  // 4. near-tie windows and the reference-order q
+  // the refinement's arguments (stages 4 and 6)
   RefArgs ra;
+  memset(&ra, 0, sizeof(ra));
   ra.ent = m->entity_embedding; ra.rel = m->relation_embedding; ra.modulus = m->modulus;
   ra.queries = queries; ra.nq = nq; ra.E = m->nentity; ra.R = m->nrelation;
   ra.Le = m->entity_dim; ra.Lr = m->relation_dim; ra.K = K; ra.c = a.c;
@@ -1049,35 +1046,107 @@ int kge_rank_filtered_ex(const kge_model_desc* m, int32_t mode, const int64_t* q
   ra.ucnt = w.ucnt; ra.ulist = w.ulist; ra.cap = RANK_CAP;
   ra.fbits = w.bits; ra.W = a.W; ra.gt = w.gt; ra.eq = w.eq; ra.gtx = w.gtx; ra.eqx = w.eqx; ra.err = err_flag;
   ra.trig = trig;
+  ra.item_off = item_off; ra.sins = sins; ra.args = args;
+  ra.lib_sin = (stage != RS_ALL) ? 1 : 0;
   // the split-bf16 tile's error bound in units of u·‖q‖·max‖e‖ (kge_rank_mfma.hip)
   const int64_t xns = xsplit_nslab(m->entity_dim);
   ra.fast_u = (rp == RP_MFMA) ? (float)(546.0 + 1.02 * xns + 0.05 * xns * 16) : 0.f;
-  st = launch_status(ops.rank_ref(mode, 0, ra, s));
-  if (st) return st;
-  // 5. fast counting pass: clear cases counted, near-ties listed
-  if (rp == RP_MFMA) {
-    st = launch_status(launch_rank_mfma_x(0, w.qs, w.es, nq, m->nentity, m->entity_dim, w.true_id, w.s_true,
-                                          w.bits, w.gt, win, s));
-  } else if (rp == RP_MFMA32) {
-    st = launch_status(launch_rank_mfma(0, w.q, m->entity_embedding, nq, m->nentity, m->entity_dim, w.true_id,
-                                        w.s_true, w.bits, w.gt, win, s));
-  } else if (rp == RP_TILE) {
-    st = launch_status(ops.rank_tile(mode, 0, ta, s));
-  } else {
-    a.prep_only = 0;
-    a.zero_counts = 0;
+  if (stage == RS_ARGS) return launch_status(ops.rank_ref(mode, 3, ra, s));
+  EmitArgs ea;
+  ea.gt = w.gt; ea.eq = w.eq; ea.gtx = w.gtx; ea.eqx = w.eqx; ea.ucnt = w.ucnt; ea.true_id = w.true_id;
+  ea.nq = nq; ea.cap = RANK_CAP; ea.ranks = ranks_out; ea.ties = ties_out; ea.listed = listed_out;
+
+  if (stage != RS_FINISH) {
     st = launch_status(ops.rank(mode, geo.vec, geo.ns, a, s));
+    if (st) return st;
+    // 2. excluded candidates (filtered ids + the true id) as a bitmap
+    st = launch_status(launch_filter_bits(filt_off, filt_ids, w.true_id, nq, m->nentity, w.bits, err_flag, s));
+    if (st) return st;
+    // the table's statistics and split operands: reused only where the tag
+    // says this workspace already holds them for this table (k_rank_tag)
+    const bool need_stats = (m->model == KGE_DISTMULT || m->model == KGE_COMPLEX || m->model == KGE_PROTATE);
+    st = launch_status(launch_rank_tag(w.tag, m->entity_embedding, m->nentity, m->entity_dim, reuse ? 1 : 0,
+                                       need_stats ? 1 : 0, rp == RP_MFMA ? 1 : 0, s));
+    if (st) return st;
+    if (need_stats) {
+      st = launch_status(launch_table_stats(m->entity_embedding, m->nentity, m->entity_dim, w.stats, s, w.tag + 5));
+      if (st) return st;
+    }
+    // 3. the fast pass's own s_true (same instruction sequence as its candidates)
+    TileArgs ta;
+    ta.q = w.q; ta.ent = m->entity_embedding; ta.modulus = m->modulus;
+    ta.nq = nq; ta.E = m->nentity; ta.Le = m->entity_dim; ta.K = K;
+    ta.c = a.c; ta.true_id = w.true_id; ta.s_true = w.s_true;
+    ta.fbits = w.bits; ta.W = a.W; ta.gt = w.gt; ta.win = win;
+    if (rp == RP_MFMA) {
+      st = launch_status(launch_split_bf16(w.q, nq, m->entity_dim, w.qs, s));
+      if (!st)
+        st = launch_status(launch_split_bf16(m->entity_embedding, m->nentity, m->entity_dim, w.es, s, w.tag + 6));
+      if (!st)
+        st = launch_status(launch_rank_mfma_x(1, w.qs, w.es, nq, m->nentity, m->entity_dim, w.true_id, w.s_true,
+                                              w.bits, w.gt, win, s));
+    } else if (rp == RP_MFMA32)
+      st = launch_status(launch_rank_mfma(1, w.q, m->entity_embedding, nq, m->nentity, m->entity_dim, w.true_id,
+                                          w.s_true, w.bits, w.gt, win, s));
+    else if (rp == RP_TILE)
+      st = launch_status(ops.rank_tile(mode, 1, ta, s));
+    if (st) return st;
+    // 4. near-tie windows and the reference-order q
+    st = launch_status(ops.rank_ref(mode, 0, ra, s));
+    if (st) return st;
+    // 5. fast counting pass: clear cases counted, near-ties listed
+    if (rp == RP_MFMA) {
+      st = launch_status(launch_rank_mfma_x(0, w.qs, w.es, nq, m->nentity, m->entity_dim, w.true_id, w.s_true,
+                                            w.bits, w.gt, win, s));
+    } else if (rp == RP_MFMA32) {
+      st = launch_status(launch_rank_mfma(0, w.q, m->entity_embedding, nq, m->nentity, m->entity_dim, w.true_id,
+                                          w.s_true, w.bits, w.gt, win, s));
+    } else if (rp == RP_TILE) {
+      st = launch_status(ops.rank_tile(mode, 0, ta, s));
+    } else {
+      a.prep_only = 0;
+      a.zero_counts = 0;
+      st = launch_status(ops.rank(mode, geo.vec, geo.ns, a, s));
+    }
+    if (st) return st;
+    if (stage == RS_LIST) {  // the lists stay in the workspace for RS_ARGS / RS_FINISH
+      ea.ranks = nullptr;
+      ea.ties = nullptr;
+      return launch_status(launch_rank_emit(ea, s));
+    }
   }
-  if (st) return st;
   // 6. refinement in the reference's operation order; exact rescan on overflow
   st = launch_status(ops.rank_ref(mode, 1, ra, s));
   if (st) return st;
   st = launch_status(ops.rank_ref(mode, 2, ra, s));
   if (st) return st;
-  EmitArgs ea;
-  ea.gt = w.gt; ea.eq = w.eq; ea.gtx = w.gtx; ea.eqx = w.eqx; ea.ucnt = w.ucnt; ea.true_id = w.true_id;
-  ea.nq = nq; ea.cap = RANK_CAP; ea.ranks = ranks_out; ea.ties = ties_out; ea.listed = listed_out;
   return launch_status(launch_rank_emit(ea, s));
+}
+}  // namespace
+}  // namespace kge
+
+extern "C" {
+
+int kge_rank_filtered_ex(const kge_model_desc* m, int32_t mode, const int64_t* queries, int64_t nq,
+                         const int64_t* filt_off, const int64_t* filt_ids, int64_t* ranks_out, int32_t* ties_out,
+                         int32_t* listed_out, int32_t path, void* workspace, size_t workspace_bytes,
+                         int32_t* err_flag, void* stream) {
+  const int stage = (path & KGE_RANK_STAGE_LIST) ? RS_LIST : RS_ALL;
+  return rank_impl(m, mode, queries, nq, filt_off, filt_ids, ranks_out, ties_out, listed_out, path, workspace,
+                   workspace_bytes, err_flag, stream, stage, nullptr, nullptr, nullptr);
+}
+
+int kge_rank_sin_args(const kge_model_desc* m, int32_t mode, int64_t nq, const int64_t* item_off, float* args_out,
+                      void* workspace, size_t workspace_bytes, int32_t* err_flag, void* stream) {
+  return rank_impl(m, mode, nullptr, nq, nullptr, nullptr, nullptr, nullptr, nullptr, RP_AUTO, workspace,
+                   workspace_bytes, err_flag, stream, RS_ARGS, item_off, nullptr, args_out);
+}
+
+int kge_rank_finish_sin(const kge_model_desc* m, int32_t mode, int64_t nq, const int64_t* item_off,
+                        const float* sin_values, int64_t* ranks_out, int32_t* ties_out, int32_t* listed_out,
+                        void* workspace, size_t workspace_bytes, int32_t* err_flag, void* stream) {
+  return rank_impl(m, mode, nullptr, nq, nullptr, nullptr, ranks_out, ties_out, listed_out, RP_AUTO, workspace,
+                   workspace_bytes, err_flag, stream, RS_FINISH, item_off, sin_values, nullptr);
 }
 
 int kge_rank_filtered(const kge_model_desc* m, int32_t mode, const int64_t* queries, int64_t nq,

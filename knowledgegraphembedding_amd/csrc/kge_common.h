@@ -28,12 +28,17 @@ int launch_rank_mfma(int gather, const float* q, const float* ent, int64_t nq, i
 // split-bf16 MFMA tile (path "mfma"): operands split once per call into bf16 hi | lo pieces
 int64_t xsplit_nslab(int K);
 int64_t xsplit_elems(int64_t rows, int K);
-int launch_split_bf16(const float* src, int64_t rows, int K, uint16_t* dst, hipStream_t s);
+int launch_split_bf16(const float* src, int64_t rows, int K, uint16_t* dst, hipStream_t s,
+                      const int64_t* skip = nullptr);
 int launch_rank_mfma_x(int gather, const uint16_t* qs, const uint16_t* es, int64_t nq, int64_t E, int K,
                        const int64_t* true_id, float* s_true, const uint32_t* bits, int32_t* gt, const RankWin& win,
                        hipStream_t s);
 constexpr int TS_BLOCKS = 1024;  // k_table_stats grid bound: stats holds 2 + 2·TS_BLOCKS floats
-int launch_table_stats(const float* ent, int64_t E, int Le, float* stats, hipStream_t s);
+int launch_table_stats(const float* ent, int64_t E, int Le, float* stats, hipStream_t s,
+                       const int64_t* skip = nullptr);
+// the ranking workspace's table tag (KGE_RANK_REUSE_TABLE; kge_rank_mfma.hip k_rank_tag)
+int launch_rank_tag(int64_t* tag, const float* ent, int64_t E, int Le, int reuse, int need_stats, int need_split,
+                    hipStream_t s);
 int launch_filter_bits(const int64_t* filt_off, const int64_t* filt_ids, const int64_t* true_id, int64_t nq,
                        int64_t E, uint32_t* bits, int32_t* err, hipStream_t s);
 struct EmitArgs {

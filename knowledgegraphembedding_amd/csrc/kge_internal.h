@@ -233,6 +233,14 @@ struct RefArgs {
   const float* trig;       // RotatE: [R, 2, Lr] reference cos | sin of the phases, or null
   float fast_u;            // > 0: the fast pass's error bound in u·‖q‖·max‖e‖ (split-bf16 tile)
   int ref_slots;           // k_rank_refine: half-waves with an LDS row slot (set by its launcher)
+  // pRotatE with the caller's sin (kge_rank_sin_args / kge_rank_finish_sin):
+  // query q's items [item_off[q], item_off[q+1]) — item 0 the true entity, then
+  // the listed candidates (or, for an overflowed window, entity ids 0..E-1) —
+  // each K phase sums (args) or their sin as the caller's library evaluates it
+  const int64_t* item_off; // [nq + 1] or null
+  const float* sins;       // [item_off[nq], K] or null (refine / exact read it)
+  float* args;             // [item_off[nq], K] (k_rank_sin_args writes it)
+  int lib_sin;             // window: the reference sin is a library's (≤ 1 ulp), not correctly rounded
 };
 
 // Register-tiled filtered ranking (kge_kernels.inc, k_rank_tile): 64 queries ×
@@ -260,7 +268,8 @@ struct ModelOps {
   int (*entity)(int mode, int vec, int ns, const EntArgs&, hipStream_t);
   int (*rank)(int mode, int vec, int ns, const RankArgs&, hipStream_t);
   int (*rank_tile)(int mode, int gather, const TileArgs&, hipStream_t);
-  // stage 0: window (δ, reference q); 1: refine the listed candidates; 2: exact rescan of overflowed queries
+  // stage 0: window (δ, reference q); 1: refine the listed candidates; 2: exact rescan of overflowed queries;
+  // 3: pRotatE phase sums of every item (k_rank_sin_args)
   int (*rank_ref)(int mode, int stage, const RefArgs&, hipStream_t);
 };
 

@@ -273,7 +273,7 @@ __global__ __launch_bounds__(256) void k_rank_emit(EmitArgs a) {
   if (q >= a.nq) return;
   const bool ok = a.true_id[q] >= 0;
   const bool ovf = a.ucnt[q] > a.cap;
-  a.ranks[q] = ok ? 1 + (int64_t)(ovf ? a.gtx[q] : a.gt[q]) : 0;
+  if (a.ranks) a.ranks[q] = ok ? 1 + (int64_t)(ovf ? a.gtx[q] : a.gt[q]) : 0;  // null: lists only
   if (a.ties) a.ties[q] = ok ? (ovf ? a.eqx[q] : a.eq[q]) : 0;
   if (a.listed) a.listed[q] = ok ? a.ucnt[q] : 0;
 }
@@ -326,7 +326,8 @@ __device__ __forceinline__ uint32_t bf16_rne(float x) {
 // as 256 contiguous bytes and, per slab, the 8 rows' hi (lo) pieces are
 // written as 256 contiguous bytes.
 __global__ __launch_bounds__(256) void k_split_bf16(const float* __restrict__ src, int64_t rows, int K, int nslab,
-                                                    int64_t nrb, uint16_t* __restrict__ dst) {
+                                                    int64_t nrb, uint16_t* __restrict__ dst, const int64_t* skip) {
+  if (skip && *skip) return;  // the workspace already holds this table's split (k_rank_tag)
   const int64_t wg = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
   const int lane = threadIdx.x & 63;
   const int nc = (nslab * XS_BK + 63) / 64;  // 64-k chunks per row
@@ -674,11 +675,11 @@ int launch_rank_mfma(int gather, const float* q, const float* ent, int64_t nq, i
 int64_t xsplit_nslab(int K) { return (K + XS_BK - 1) / XS_BK; }
 int64_t xsplit_elems(int64_t rows, int K) { return ((rows + 127) / 128) * 128 * xsplit_nslab(K) * XS_BK * 2; }
 
-int launch_split_bf16(const float* src, int64_t rows, int K, uint16_t* dst, hipStream_t s) {
+int launch_split_bf16(const float* src, int64_t rows, int K, uint16_t* dst, hipStream_t s, const int64_t* skip) {
   const int64_t nrb = (rows + 127) / 128, nslab = xsplit_nslab(K);
   const int64_t waves = nrb * 16 * ((nslab * XS_BK + 63) / 64);  // 8 rows × 64 k each
   hipLaunchKernelGGL(k_split_bf16, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s, src, rows, K, (int)nslab,
-                     nrb, dst);
+                     nrb, dst, skip);
   return (int)hipGetLastError();
 }
 
@@ -725,7 +726,8 @@ int launch_rank_mfma_x(int gather, const uint16_t* qs, const uint16_t* es, int64
 // the 35 µs pass; per row, 0.93 ms).  stats needs 2 + 2·TS_BLOCKS floats.
 constexpr int TS_ROWS = 4;
 __global__ __launch_bounds__(256) void k_table_stats(const float* __restrict__ ent, int64_t E, int Le,
-                                                     float* stats) {
+                                                     float* stats, const int64_t* skip) {
+  if (skip && *skip) return;  // still valid in the workspace (k_rank_tag)
   __shared__ float red[2][4];
   const int lane = threadIdx.x & 63, w = wave_id();
   const bool vec4 = (Le & 3) == 0 && (((uintptr_t)ent) & 15) == 0;
@@ -770,7 +772,8 @@ __global__ __launch_bounds__(256) void k_table_stats(const float* __restrict__ e
   }
 }
 
-__global__ __launch_bounds__(256) void k_stats_reduce(float* stats, int nblocks) {
+__global__ __launch_bounds__(256) void k_stats_reduce(float* stats, int nblocks, const int64_t* skip) {
+  if (skip && *skip) return;
   __shared__ float red[2][4];
   const int lane = threadIdx.x & 63, w = wave_id();
   float n = 0.f, m = 0.f;
@@ -791,13 +794,41 @@ __global__ __launch_bounds__(256) void k_stats_reduce(float* stats, int nblocks)
   }
 }
 
-int launch_table_stats(const float* ent, int64_t E, int Le, float* stats, hipStream_t s) {
+int launch_table_stats(const float* ent, int64_t E, int Le, float* stats, hipStream_t s, const int64_t* skip) {
   const int64_t want = (E + 4 * TS_ROWS - 1) / (4 * TS_ROWS);
   const int blocks = (int)(want < TS_BLOCKS ? (want > 0 ? want : 1) : TS_BLOCKS);
-  hipLaunchKernelGGL(k_table_stats, dim3((unsigned)blocks), dim3(256), 0, s, ent, E, Le, stats);
+  hipLaunchKernelGGL(k_table_stats, dim3((unsigned)blocks), dim3(256), 0, s, ent, E, Le, stats, skip);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return (int)e;
-  hipLaunchKernelGGL(k_stats_reduce, dim3(1), dim3(256), 0, s, stats, blocks);
+  hipLaunchKernelGGL(k_stats_reduce, dim3(1), dim3(256), 0, s, stats, blocks, skip);
+  return (int)hipGetLastError();
+}
+
+// The ranking workspace's table tag (KGE_RANK_REUSE_TABLE): tag = [entity
+// pointer, nentity, entity_dim, statistics valid, split valid, skip statistics,
+// skip split, -].  With reuse requested, the statistics / split operands a
+// previous call left are reused only if that call ranked the same table
+// pointer and shape and actually wrote them (a scan- or tile-path call writes
+// no split; a DistMult call after a RotatE one finds no statistics); the tag
+// then describes what this call leaves behind.  One thread, stream-ordered
+// before the kernels that read the skip words.
+__global__ void k_rank_tag(int64_t* tag, const float* ent, int64_t E, int Le, int reuse, int need_stats,
+                           int need_split) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  const bool match = reuse && tag[0] == (int64_t)(uintptr_t)ent && tag[1] == E && tag[2] == Le;
+  const int64_t sv = match ? tag[3] : 0, xv = match ? tag[4] : 0;
+  tag[5] = (need_stats && sv) ? 1 : 0;
+  tag[6] = (need_split && xv) ? 1 : 0;
+  tag[0] = (int64_t)(uintptr_t)ent;
+  tag[1] = E;
+  tag[2] = Le;
+  tag[3] = need_stats ? 1 : sv;
+  tag[4] = need_split ? 1 : xv;
+}
+
+int launch_rank_tag(int64_t* tag, const float* ent, int64_t E, int Le, int reuse, int need_stats, int need_split,
+                    hipStream_t s) {
+  hipLaunchKernelGGL(k_rank_tag, dim3(1), dim3(64), 0, s, tag, ent, E, Le, reuse, need_stats, need_split);
   return (int)hipGetLastError();
 }
 

@@ -21,10 +21,13 @@
 // vectorized CPU transcendentals cannot be reproduced on the device, so
 // RotatE's cos / sin of the relation phases come from a table the caller
 // evaluated with the reference's own ATen op (kge_model_desc.relation_trig);
-// without one — and always for pRotatE's sin of per-candidate phase sums —
-// correctly rounded values are used (double evaluation rounded once), which
-// differ from the reference's in the last bit on a few percent of arguments
-// (DESIGN.md §5).
+// without one correctly rounded values are used (double evaluation rounded
+// once), which differ from the reference's in the last bit on a few percent of
+// arguments.  pRotatE's sin acts on per-candidate phase sums, so
+// no table can carry it: the caller evaluates the sin of exactly the phase
+// sums the refinement needs with the reference's own library call
+// (kge_rank_sin_args → host → kge_rank_finish_sin), and the SIN form of
+// ref_score_half sums those values; without them, correctly rounded sin.
 #pragma once
 #include "kge_device.h"
 
@@ -104,11 +107,14 @@ __device__ __forceinline__ float half_shfl(float v, int src_hl) {
 // Reference-order score of the candidate row e against the query's reference
 // q, computed by one 32-lane half-wave (hl = lane within the half); every
 // lane of the half returns the score.  q / e: [K] real, or [re K | im K].
-template <int M, int MODE>
+// SIN (pRotatE): e holds the K values sin(phase sum) as the caller's library
+// evaluated them; the element is their abs (model.py:245-246), q is unused.
+template <int M, int MODE, bool SIN = false>
 __device__ float ref_score_half(const float* __restrict__ q, const float* __restrict__ e, int K, const Consts& c,
                                 int hl) {
   constexpr bool CPLX = Traits<M>::cplx;
   auto elem = [&](int k) -> float {
+    if constexpr (SIN) return fabsf(e[k]);
     const float qa = q[k], ea = e[k];
     const float qb = CPLX ? q[K + k] : 0.f, eb = CPLX ? e[K + k] : 0.f;
     return ref_elem<M, MODE>(qa, qb, ea, eb, c);

@@ -93,6 +93,7 @@ kge_model_desc make_desc(int64_t model, const Tensor& entity, const Tensor& rela
   check_table(relation, "relation_embedding");
   kge_model_desc d;
   std::memset(&d, 0, sizeof(d));
+  d.struct_size = (int32_t)sizeof(d);
   d.model = (int32_t)model;
   d.entity_dim = (int32_t)entity.size(1);
   d.relation_dim = (int32_t)relation.size(1);
@@ -319,10 +320,39 @@ std::tuple<Tensor, Tensor> rank_filtered_cuda(const Tensor& entity, const Tensor
   Tensor ties = at::empty({nq}, at::TensorOptions().dtype(at::kInt).device(dev));
   if (nq == 0) return {ranks, ties};
   Tensor ws = workspace(kge_rank_workspace_bytes(&d, nq), dev);
+  int32_t* err = error_flag_for(dev).data_ptr<int32_t>();
+  void* st = current_stream(dev);
+  if (model == KGE_PROTATE) {
+    // bit-exact pRotatE (kge_hip.h, three-call form): the near-ties' phase
+    // sums go through the reference's own sin — ATen's CPU at::sin, the call
+    // model.py:245 makes — and come back for the reference-order re-scoring
+    Tensor cnt = at::empty({nq}, at::TensorOptions().dtype(at::kInt).device(dev));
+    check_status(kge_rank_filtered_ex(&d, (int32_t)mode, q.data_ptr<int64_t>(), nq, off.data_ptr<int64_t>(),
+                                      ids.data_ptr<int64_t>(), ranks.data_ptr<int64_t>(), ties.data_ptr<int32_t>(),
+                                      cnt.data_ptr<int32_t>(), (int32_t)path | KGE_RANK_STAGE_LIST, ws.data_ptr(),
+                                      (size_t)ws.numel(), err, st),
+                 "kge_rank_filtered_ex (list)");
+    const Tensor c = cnt.to(at::kCPU);  // sync: the counts size the argument buffer
+    Tensor item_off = at::empty({nq + 1}, at::TensorOptions().dtype(at::kLong));
+    int64_t* io = item_off.data_ptr<int64_t>();
+    const int32_t* cp = c.data_ptr<int32_t>();
+    io[0] = 0;
+    for (int64_t i = 0; i < nq; ++i) io[i + 1] = io[i] + 1 + (cp[i] > KGE_RANK_LIST_CAP ? d.nentity : cp[i]);
+    const Tensor off_d = item_off.to(dev);
+    Tensor args = at::empty({io[nq], (int64_t)d.entity_dim}, entity.options());
+    check_status(kge_rank_sin_args(&d, (int32_t)mode, nq, off_d.data_ptr<int64_t>(), args.data_ptr<float>(),
+                                   ws.data_ptr(), (size_t)ws.numel(), err, st),
+                 "kge_rank_sin_args");
+    const Tensor sins = at::sin(args.to(at::kCPU)).to(dev);
+    check_status(kge_rank_finish_sin(&d, (int32_t)mode, nq, off_d.data_ptr<int64_t>(), sins.data_ptr<float>(),
+                                     ranks.data_ptr<int64_t>(), ties.data_ptr<int32_t>(), nullptr, ws.data_ptr(),
+                                     (size_t)ws.numel(), err, st),
+                 "kge_rank_finish_sin");
+    return {ranks, ties};
+  }
   check_status(kge_rank_filtered_ex(&d, (int32_t)mode, q.data_ptr<int64_t>(), nq, off.data_ptr<int64_t>(),
                                     ids.data_ptr<int64_t>(), ranks.data_ptr<int64_t>(), ties.data_ptr<int32_t>(),
-                                    nullptr, (int32_t)path, ws.data_ptr(), (size_t)ws.numel(),
-                                    error_flag_for(dev).data_ptr<int32_t>(), current_stream(dev)),
+                                    nullptr, (int32_t)path, ws.data_ptr(), (size_t)ws.numel(), err, st),
                "kge_rank_filtered_ex");
   return {ranks, ties};
 }

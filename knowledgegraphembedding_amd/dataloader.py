@@ -167,6 +167,8 @@ class RankShardSampler(torch.utils.data.Sampler):
     def __init__(self, n: int, rank: int, world: int, seed: int):
         if world < 1 or not 0 <= rank < world:
             raise ValueError(f"rank {rank} outside world {world}")
+        if n < world:  # every rank's shard would be empty: the DataLoader would yield nothing, forever
+            raise ValueError(f"{n} training triples cannot be sharded over {world} ranks")
         self.n, self.rank, self.world, self.seed = int(n), int(rank), int(world), int(seed)
         self.epoch = 0
 

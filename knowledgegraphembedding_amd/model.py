@@ -230,11 +230,13 @@ class KGEModel(nn.Module):
         self.keep_grads = True
         # apply a KGEAdam update inside the gradient passes (kge_train_step)
         self.fuse_optimizer = True
-        # RotatE ranking: rotate the queries by the reference's own CPU cos /
-        # sin of the relation phases ("reference", ops.reference_rotation:
-        # ranks bit-exact to the reference's), or by correctly rounded values
-        # evaluated on the device ("device": no host work, last-bit trig
-        # differences can move a near-tied rank)
+        # RotatE / pRotatE ranking: the reference's own CPU trig ("reference":
+        # RotatE's queries rotated by its cos / sin of the relation phases,
+        # ops.reference_rotation; pRotatE's near-ties re-scored from its sin
+        # of their phase sums, ops.reference_sin — ranks bit-exact to the
+        # reference's), or correctly rounded values evaluated on the device
+        # ("device": no host work, last-bit trig differences can move a
+        # near-tied rank)
         self.rank_trig = "reference"
 
     # ------------------------------------------------------------------ helpers
@@ -265,6 +267,15 @@ class KGEModel(nn.Module):
                 raise ValueError("rank_trig %s not supported" % self.rank_trig)
             relation_trig = ops.reference_rotation(self.relation_embedding, self._host_scalars()[1])
         return relation_trig.to(dev, torch.float32).contiguous()
+
+    def _rank_library_sin(self):
+        """pRotatE: re-score the ranking's near-ties with the reference's own
+        host sin (ops.reference_sin), per `rank_trig`."""
+        if self.model_name != 'pRotatE':
+            return False
+        if self.rank_trig not in ("reference", "device"):
+            raise ValueError("rank_trig %s not supported" % self.rank_trig)
+        return self.rank_trig == "reference"
 
     def desc(self):
         """The C-ABI model descriptor, rebuilt only when a table moves or is replaced."""
@@ -516,6 +527,7 @@ class KGEModel(nn.Module):
         per_mode = []  # device rank tensors; read back once, after both directions are queued
         with torch.no_grad():
             trig = model._rank_rotation(dev)
+            lsin = model._rank_library_sin()
             for mode in ('head-batch', 'tail-batch'):
                 ranks_all = []
                 per_mode.append(ranks_all)
@@ -524,7 +536,7 @@ class KGEModel(nn.Module):
                     off, ids = index.filter_csr(q, mode)
                     ranks, _ = ops.rank_filtered(desc, mode, torch.from_numpy(q), torch.from_numpy(off),
                                                  torch.from_numpy(ids), dev, relation_trig=trig,
-                                                 reuse_table=step > 0)
+                                                 reuse_table=step > 0, library_sin=lsin)
                     ranks_all.append(ranks)
                     # progress messages on the reference's batch cadence
                     nb = (len(q) + test_batch_size - 1) // test_batch_size
@@ -573,7 +585,8 @@ class KGEModel(nn.Module):
                 if qd is None:
                     qd, flat = flat[:3 * nq].view(nq, 3), flat[3 * nq:]
                 outs.append(ops.rank_filtered(self.desc(), mode, qd, flat[:nq + 1], flat[nq + 1:], dev, path=path,
-                                              relation_trig=trig, reuse_table=bool(outs)))
+                                              relation_trig=trig, reuse_table=bool(outs),
+                                              library_sin=self._rank_library_sin()))
             # one device → host copy (pinned): both directions' ranks (int64 as
             # int32 pairs) and ties, and the error flag
             packed = torch.cat([outs[0][0].view(torch.int32), outs[1][0].view(torch.int32), outs[0][1], outs[1][1],
@@ -600,7 +613,8 @@ class KGEModel(nn.Module):
         with torch.no_grad():
             out = ops.rank_filtered(self.desc(), mode, torch.from_numpy(q), torch.from_numpy(off),
                                     torch.from_numpy(ids), dev, path=path, listed=listed,
-                                    relation_trig=self._rank_rotation(dev, relation_trig))
+                                    relation_trig=self._rank_rotation(dev, relation_trig),
+                                    library_sin=self._rank_library_sin())
         res = tuple(t.cpu().numpy() for t in out)
         ops.raise_on_device_error(dev)
         return res

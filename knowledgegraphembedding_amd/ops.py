@@ -9,6 +9,7 @@ from __future__ import annotations
 import math
 from typing import Optional
 
+import numpy as np
 import torch
 
 from . import _lib
@@ -97,6 +98,8 @@ def raise_device_error_value(dev: torch.device, v: int) -> None:
         if v & _lib.DEVERR_SAMPLER:
             raise RuntimeError("negative sampler: a positive's true heads/tails leave too few candidate "
                                "entities (the reference's sampling loop would not terminate)")
+        if v & _lib.DEVERR_ARG:
+            raise RuntimeError("kge_rank_sin_args: item offsets do not match the listed near-tie counts")
         raise RuntimeError(f"device error flag {v}")
 
 
@@ -417,7 +420,8 @@ RANK_REUSE_TABLE = 0x100  # kge_hip.h KGE_RANK_REUSE_TABLE
 
 def rank_filtered(desc: _lib.ModelDesc, mode: str, queries: torch.Tensor, filt_off: torch.Tensor,
                   filt_ids: torch.Tensor, dev, path: str = "auto", listed: bool = False,
-                  relation_trig: Optional[torch.Tensor] = None, reuse_table: bool = False):
+                  relation_trig: Optional[torch.Tensor] = None, reuse_table: bool = False,
+                  library_sin: bool = False):
     """Filtered ranks (int64) and tie counts (int32) for a block of queries
     (model.py:383-418), in the reference's fp32 score order
     (kge_rank_filtered_ex).  `path` picks the fast counting pass ("auto",
@@ -428,7 +432,10 @@ def rank_filtered(desc: _lib.ModelDesc, mode: str, queries: torch.Tensor, filt_o
     earlier call on this device ranked the same model with the same, unchanged
     entity table (the other direction or another query block of one
     evaluation) — its table statistics and split operands are reused when the
-    shared workspace is still the same buffer (else recomputed)."""
+    shared workspace is still the same buffer (else recomputed).
+    `library_sin` (pRotatE): evaluate the sin of the near-ties' phase sums
+    with the reference's own torch.sin on the host (reference_sin), so the
+    ranks are the reference's bit for bit; False: correctly rounded device sin."""
     if mode not in ("head-batch", "tail-batch"):
         raise ValueError("mode %s not supported" % mode)
     if path not in RANK_PATHS:
@@ -450,19 +457,64 @@ def rank_filtered(desc: _lib.ModelDesc, mode: str, queries: torch.Tensor, filt_o
     lib = _lib.load()
     need = lib.kge_rank_workspace_bytes(desc, nq)
     st = state(dev)
-    prev = st.rank_ws_ptr  # the last ranking call's buffer, cleared by any other workspace user
+    key = (desc.entity_embedding, desc.nentity, desc.entity_dim, desc.model)
+    prev = st.rank_ws_ptr  # the last ranking call's (buffer, table), cleared by any other workspace user
     ws = st.workspace(need)
     # the table's statistics / split operands survive only in the same buffer
-    reuse_table = reuse_table and prev == ws.data_ptr()
-    st.rank_ws_ptr = ws.data_ptr()
-    _lib.check(
-        lib.kge_rank_filtered_ex(desc, _lib.MODE_IDS[mode], q.data_ptr(), nq, off.data_ptr(), ids.data_ptr(),
-                                 ranks.data_ptr(), ties.data_ptr(), _ptr(lst),
-                                 RANK_PATHS[path] | (RANK_REUSE_TABLE if reuse_table else 0), ws.data_ptr(),
-                                 ws.numel(), st.err.data_ptr(), _stream(dev)),
-        "kge_rank_filtered_ex",
-    )
+    # (the library also checks its own tag of what the buffer holds)
+    reuse_table = reuse_table and prev == (ws.data_ptr(),) + key
+    st.rank_ws_ptr = (ws.data_ptr(),) + key
+    flags = RANK_PATHS[path] | (RANK_REUSE_TABLE if reuse_table else 0)
+    mode_id = _lib.MODE_IDS[mode]
+    if library_sin and desc.model == _lib.MODEL_IDS["pRotatE"] and nq:
+        _rank_protate_library_sin(lib, desc, mode_id, q, nq, off, ids, ranks, ties, lst, flags, ws, st, dev)
+    else:
+        _lib.check(
+            lib.kge_rank_filtered_ex(desc, mode_id, q.data_ptr(), nq, off.data_ptr(), ids.data_ptr(),
+                                     ranks.data_ptr(), ties.data_ptr(), _ptr(lst), flags, ws.data_ptr(),
+                                     ws.numel(), st.err.data_ptr(), _stream(dev)),
+            "kge_rank_filtered_ex",
+        )
     return (ranks, ties, lst) if listed else (ranks, ties)
+
+
+def reference_sin(args: torch.Tensor) -> torch.Tensor:
+    """sin of pRotatE phase sums as the reference evaluates them: its own
+    `torch.sin` on the CPU (model.py:245; ATen's vectorized CPU kernel — MKL
+    VML in this build — whose last bits no device instruction sequence
+    reproduces).  Elementwise, so the values do not depend on how the
+    arguments are batched (tests/test_rank_parity_gpu.py checks this host's
+    bits against the reference's, tests/golden/protate_sin.npz)."""
+    return torch.sin(args)
+
+
+def _rank_protate_library_sin(lib, desc, mode_id, q, nq, off, ids, ranks, ties, lst, flags, ws, st, dev):
+    """pRotatE ranks bit-exact to the reference (kge_hip.h: the three-call
+    form): the device lists each query's near-ties, writes the phase sums of
+    the true entity and every listed candidate; the host takes their sin with
+    the reference's own call; the device re-scores them in the reference's
+    order.  One host round trip per call (sync), ≈ items × K × 4 bytes each
+    way (wn18rr, K = 500: ≈ 260 listed per query → ≈ 0.5 MB per query)."""
+    cnt = torch.empty(nq, dtype=torch.int32, device=dev)
+    wsp, wsn, err, s = ws.data_ptr(), ws.numel(), st.err.data_ptr(), _stream(dev)
+    _lib.check(lib.kge_rank_filtered_ex(desc, mode_id, q.data_ptr(), nq, off.data_ptr(), ids.data_ptr(),
+                                        ranks.data_ptr(), ties.data_ptr(), cnt.data_ptr(),
+                                        flags | _lib.RANK_STAGE_LIST, wsp, wsn, err, s),
+               "kge_rank_filtered_ex (list)")
+    c = cnt.cpu().numpy().astype(np.int64)  # sync: the item counts size the argument buffer
+    items = np.where(c > _lib.RANK_LIST_CAP, 1 + int(desc.nentity), 1 + c)
+    item_off = np.zeros(nq + 1, dtype=np.int64)
+    np.cumsum(items, out=item_off[1:])
+    K = int(desc.entity_dim)
+    off_d = torch.from_numpy(item_off).to(dev)
+    args = torch.empty((int(item_off[-1]), K), dtype=torch.float32, device=dev)
+    _lib.check(lib.kge_rank_sin_args(desc, mode_id, nq, off_d.data_ptr(), args.data_ptr(), wsp, wsn, err, s),
+               "kge_rank_sin_args")
+    sins = reference_sin(args.cpu()).to(dev)
+    del args
+    _lib.check(lib.kge_rank_finish_sin(desc, mode_id, nq, off_d.data_ptr(), sins.data_ptr(), ranks.data_ptr(),
+                                       ties.data_ptr(), _ptr(lst), wsp, wsn, err, s),
+               "kge_rank_finish_sin")
 
 
 def sample_negatives(triples: torch.Tensor, batch: torch.Tensor, nentity: int, negative_sample_size: int,

@@ -123,6 +123,8 @@ class DeviceTrainIterator:
         self.seed = int(seed)
         if world < 1 or not 0 <= rank < world:
             raise ValueError(f"rank {rank} outside world {world}")
+        if self.triples.shape[0] < world:  # each rank's epoch shard would be empty: endless empty batches
+            raise ValueError(f"{self.triples.shape[0]} training triples cannot be sharded over {world} ranks")
         self.rank, self.world = int(rank), int(world)
         self.gen = torch.Generator(device=dev)
         self.gen.manual_seed(self.seed if perm_seed is None else int(perm_seed))

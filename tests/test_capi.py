@@ -85,3 +85,37 @@ def test_python_errors_match_reference():
         ops.make_desc("Foo", torch.zeros(2, 2), torch.zeros(2, 2), 1.0, 1.0, None)
     with pytest.raises(RuntimeError, match="ROCm"):
         ops._require_device(torch.zeros(2))
+
+
+def test_abi_version_and_struct_size():
+    """a caller built against another kge_model_desc layout is
+    refused (KGE_ERR_ABI) instead of reading past its struct; the loader
+    refuses a library of another ABI version."""
+    lib = _lib.load()
+    assert lib.kge_version().decode().split()[1] == _lib.ABI_VERSION
+    d, _buf = _desc()
+    assert d.struct_size == C.sizeof(_lib.ModelDesc)
+    out = (C.c_float * 4)()
+    p = C.cast(out, C.c_void_p)
+    d.struct_size = C.sizeof(_lib.ModelDesc) - 8  # an older, shorter struct
+    st = lib.kge_score(C.byref(d), 2, p, p, 1, 1, p, p, None)
+    assert st == 7 and b"struct_size" in lib.kge_status_string(st)
+    d.struct_size = 0  # the round-3 layout's "reserved" word
+    assert lib.kge_rank_workspace_bytes(C.byref(d), 4) > 0  # (sizes only; no validation there)
+    assert lib.kge_rank_filtered(C.byref(d), 2, p, 1, p, p, p, p, p, 1 << 20, p, None) == 7
+
+
+def test_protate_library_sin_stage_checks():
+    """The three-call pRotatE form accepts only pRotatE and needs its buffers
+    (checked on the host before any launch)."""
+    lib = _lib.load()
+    p = C.cast((C.c_float * 4)(), C.c_void_p)
+    d, _buf = _desc(3, 16, 8)  # RotatE
+    assert lib.kge_rank_sin_args(C.byref(d), 2, 1, p, p, p, 1 << 20, p, None) == 1
+    assert lib.kge_rank_finish_sin(C.byref(d), 2, 1, p, p, p, p, None, p, 1 << 20, p, None) == 1
+    d, _buf = _desc(4, 16, 16)  # pRotatE
+    assert lib.kge_rank_sin_args(C.byref(d), 2, 1, None, p, p, 1 << 20, p, None) == 4
+    assert lib.kge_rank_finish_sin(C.byref(d), 2, 1, p, None, p, p, None, p, 1 << 20, p, None) == 4
+    assert lib.kge_rank_filtered_ex(C.byref(d), 2, p, 1, p, p, p, p, None, _lib.RANK_STAGE_LIST, p, 1 << 20, p,
+                                    None) == 4  # the list stage must return the counts
+    assert lib.kge_rank_sin_args(C.byref(d), 2, 1, p, p, p, 16, p, None) == 5  # workspace

@@ -1,38 +1,42 @@
-"""Filtered-rank parity with the reference: the HIP ranking
-against ranks the reference's own test_step produced (tests/golden/
+"""Filtered-rank parity with the reference: the HIP
+ranking against ranks the reference's own test_step produced (tests/golden/
 make_golden.py: `ranks` on synthetic KGs, `ranks_full` at config-3 scale — the
 real wn18rr split with DistMult / ComplEx / pRotatE at d = 500 and E = 40943,
-the FB15k entity set with TransE / RotatE at d = 1000).
+512 queries per direction, the FB15k entity set with TransE / RotatE at
+d = 1000).
 
 What is asserted, per query (rank = 1 + #{unfiltered e ≠ true: s_e > s_true}):
-  * TransE, DistMult, ComplEx, RotatE: the kernel's near-ties are re-scored in
-    the reference's fp32 operation order (kge_rank_ref.h), so ranks AND tie
-    counts equal the reference's on every query; where the reference has exact
-    ties (its argsort is not stable) its position lies in [rank, rank + ties].
+  * all five models: the kernel's near-ties are re-scored in the reference's
+    fp32 operation order (kge_rank_ref.h), so ranks AND tie counts equal the
+    reference's on every query (0 untied disagreements); where the reference
+    has exact ties (its argsort is not stable) its position lies in
+    [rank, rank + ties].
     RotatE's rotation comes from the reference's own cos / sin bits of the
     relation phases (tests/golden/rotate_trig.npz, made by the reference's
     ATen CPU ops in make_golden.py `gen_rotate_trig`), fed to the kernels as
     kge_model_desc.relation_trig — the table KGEModel builds itself with
     ops.reference_rotation on the host it runs on.
-  * pRotatE: its sin acts on per-candidate phase sums (model.py:241-245), so
-    no table can carry the reference's values; correctly rounded sin here.  A
-    query is decidable when no competitor of the reference lies within the
-    rigorous bound δ of what last-bit sin differences can move a gap (below);
-    decidable queries must match exactly, the others within the number of
-    competitors inside δ, and at most 5 % of the untied queries may differ.
+    pRotatE's sin acts on per-candidate phase sums (model.py:241-245): the
+    device lists the near-ties, writes their phase sums, the host takes the
+    sin with the reference's own torch.sin (ops.reference_sin), and the device
+    re-scores them (kge_rank_sin_args / kge_rank_finish_sin).
+  * pRotatE with correctly rounded DEVICE sin (rank_trig = "device"): equal on
+    every query decidable under the rigorous last-bit-of-sin bound δ below,
+    within the competitors inside δ otherwise.
   * Every fast path (split-bf16 MFMA tile = "auto" for DistMult / ComplEx,
     fp32 MFMA tile, register tile, wave scan) returns the same ranks and ties
     bit for bit: their windows differ, the refinement does not.
-  * test_host_trig_matches_reference: this host's torch.cos / torch.sin (what
-    KGEModel.test_step uses) against the reference's committed bits; if they
-    differ, the reference's RotatE ranks depend on the CPU's vector library,
-    and the test reports by how much (ranks from this host's table against
-    the reference's).
+  * test_host_trig_matches_reference / test_host_sin_matches_reference: this
+    host's torch.cos / torch.sin (what KGEModel.test_step uses) against the
+    reference's committed bits, and that torch.sin's bits do not depend on how
+    its input is batched (the reference takes the sin of a [B, E, d] tensor,
+    the ranking of a [items, d] one).
 
-δ for pRotatE (u = 2^-24, K dims, S = (γ − s_true)/mod): |sin| moves by ≤ u per
-element; every partial sum of the reference's reduction (≤ K/32 + 24 per lane
-column and fold) may round the other way by ≤ 2u of its value; both the
-candidate and the true score move:  δ = 2·mod·(K·u + (4 + 2·(K/32 + 24))·u·S).
+δ for pRotatE with device sin (u = 2^-24, K dims, S = (γ − s_true)/mod): |sin|
+moves by ≤ u per element; every partial sum of the reference's reduction
+(≤ K/32 + 24 per lane column and fold) may round the other way by ≤ 2u of its
+value; both the candidate and the true score move:
+δ = 2·mod·(K·u + (4 + 2·(K/32 + 24))·u·S).
 """
 import numpy as np
 import pytest
@@ -44,7 +48,7 @@ from knowledgegraphembedding_amd import KGEModel
 pytestmark = pytest.mark.gpu
 DEV = torch.device("cuda", 0)
 U = 2.0 ** -24
-EXACT = ("TransE", "DistMult", "ComplEx", "RotatE")
+EXACT = ("TransE", "DistMult", "ComplEx", "RotatE", "pRotatE")
 PATHS = {"DistMult": ("auto", "mfma32", "tile", "scan"), "ComplEx": ("auto", "mfma32", "tile", "scan"),
          "TransE": ("auto", "scan"), "RotatE": ("auto", "scan"), "pRotatE": ("auto", "scan")}
 
@@ -74,9 +78,9 @@ def reference_trig(tag, rel, rng):
     return torch.from_numpy(np.stack([cs, sn], 1)), phase, ids
 
 
-def trig_bound(name, mod, queries, d, gamma, s_true):
+def trig_bound(name, mod, queries, d, gamma, s_true, exact=True):
     """δ above (0 for the models whose operations are all reproduced)."""
-    if name in EXACT:
+    if exact:
         return np.zeros(len(queries))
     K = d
     fold = 4 + 2 * (K / 32 + 24)
@@ -85,14 +89,14 @@ def trig_bound(name, mod, queries, d, gamma, s_true):
     return 2 * m * (K * U + fold * U * S)
 
 
-def check(tag, name, mode, ranks, ties, ref, bound):
+def check(tag, name, mode, ranks, ties, ref, bound, exact=True):
     """The assertions of the module docstring; returns (decidable, differing, ambiguous)."""
     r_rank, r_ties, gaps = ref["rank"].astype(np.int64), ref["ties"], ref["gap"]
     near = (np.abs(gaps) <= bound[:, None]).sum(1)
     decidable = (r_ties == 0) & (near == 0)
     bad = decidable & (ranks != r_rank)
     assert not bad.any(), f"{tag} {name} {mode}: queries {np.nonzero(bad)[0][:8]} {ranks[bad][:8]} vs {r_rank[bad][:8]}"
-    if name in EXACT:
+    if exact:
         assert np.array_equal(ties, r_ties), f"{tag} {name} {mode}: tie counts differ"
         assert np.all((r_rank >= ranks) & (r_rank <= ranks + ties)), f"{tag} {name} {mode}: tie interval"
     else:
@@ -101,9 +105,10 @@ def check(tag, name, mode, ranks, ties, ref, bound):
     differ = ranks != r_rank
     # a query the reference ties at the true score is placed by its non-stable
     # argsort somewhere in [rank, rank + ties] (checked above); the others may
-    # differ only through pRotatE's sin bound, and on at most 5 % of the queries
+    # differ only through device sin's bound (pRotatE, rank_trig "device"), on
+    # at most 5 % of the queries
     untied_differ = int((differ & (r_ties == 0)).sum())
-    cap = 0 if name in EXACT else 0.05 * len(ranks)
+    cap = 0 if exact else 0.05 * len(ranks)
     assert untied_differ <= cap, f"{tag} {name} {mode}: {untied_differ} of {len(ranks)} ranks differ"
     return int(decidable.sum()), int((r_ties > 0).sum()), int((~decidable).sum()), int(differ.sum()), untied_differ
 
@@ -126,6 +131,14 @@ def run_case(tag, name, E, R, d, gamma, seed, queries, filters, refs, report):
             dec, tied, amb, diff, udiff = check(tag, name, mode, ranks, ties, ref, bound)
             report.append((tag, name, mode, path, nq, dec, tied, amb, diff, udiff, round(float(listed.mean()), 1),
                            int(listed.max())))
+        if name == "pRotatE":  # correctly rounded device sin: within the last-bit bound
+            m.rank_trig = "device"
+            ranks, ties, listed = m.rank_queries(qs, filters, mode, listed=True)
+            m.rank_trig = "reference"
+            bound = trig_bound(name, mod, qs, d, gamma, ref["s_true"], exact=False)
+            dec, tied, amb, diff, udiff = check(tag, name, mode, ranks, ties, ref, bound, exact=False)
+            report.append((tag, name, mode, "auto/device-sin", nq, dec, tied, amb, diff, udiff,
+                           round(float(listed.mean()), 1), int(listed.max())))
     del m
     torch.cuda.empty_cache()
 
@@ -213,6 +226,41 @@ def test_host_trig_matches_reference(g_full, golden_info, capsys):
         with capsys.disabled():
             print(f"  {mode}: ranks from this host's cos/sin differ from the reference's on "
                   f"{int((ranks != r_rank).sum())} of {nq} queries")
+
+
+def test_host_sin_matches_reference(golden_info, g_full, capsys):
+    """pRotatE: this host's torch.sin (ops.reference_sin, what the ranking's
+    near-ties are re-scored from) on the true entities' phase sums of the
+    first 128 wn18rr fixture queries, both associations (model.py:240-243),
+    against the reference's bits (tests/golden/protate_sin.npz); and the same
+    values from the arguments batched differently (a permuted [items, d] block
+    and odd-length slices, as the ranking batches them) — the reference took
+    the sin of a [B, E, d] tensor."""
+    from knowledgegraphembedding_amd import ops
+    info = golden_info["protate_sin"]
+    E, R, d, gamma, seed, nq = (info[k] for k in ("E", "R", "d", "gamma", "seed", "queries"))
+    ent, rel, _, rng = synth_tables("pRotatE", E, R, d, torch.Tensor([gamma]).item(), seed)
+    q = torch.from_numpy(g_full["wn18rr/queries"][:nq])
+    div = rng / 3.14159262358979323846  # model.py:232-238 (a Python float, as the reference's)
+    ph = torch.from_numpy(ent)[q[:, 0]] / div
+    pr = torch.from_numpy(rel)[q[:, 1]] / div
+    pt = torch.from_numpy(ent)[q[:, 2]] / div
+    args = torch.stack([ph + (pr - pt), (ph + pr) - pt])
+    mine = ops.reference_sin(args).numpy()
+    cr = np.sin(args.numpy().astype(np.float64)).astype(np.float32)
+    ref = (cr.view(np.uint32) ^ load_npz("protate_sin.npz")["sin_xor"]).view(np.float32)
+    differ = float((mine.view(np.uint32) != ref.view(np.uint32)).mean())
+    flat = args.reshape(-1)
+    perm = torch.from_numpy(np.random.default_rng(3).permutation(flat.numel()))
+    batched = torch.empty_like(flat)
+    batched[perm] = ops.reference_sin(flat[perm].contiguous())
+    for a0, n in ((1, 7), (13, 501), (1000, 4099)):
+        assert torch.equal(ops.reference_sin(flat[a0:a0 + n].clone()), batched[a0:a0 + n])
+    with capsys.disabled():
+        print(f"\nhost torch.sin vs the reference's bits on {mine.size} pRotatE phase sums: {differ:.4%} differ "
+              f"(MKL {torch.backends.mkl.is_available()}, cpu capability {torch.backends.cpu.get_cpu_capability()})")
+    assert torch.equal(batched.view(mine.shape), torch.from_numpy(mine)), "torch.sin depends on the batching"
+    assert differ == 0.0, "this host's sin differs from the reference's: pRotatE ranks would follow this host's"
 
 
 @pytest.mark.parametrize("name,E,d", [("DistMult", 300, 50), ("DistMult", 257, 37), ("DistMult", 1000, 130),

@@ -1,0 +1,129 @@
+"""Every data-parallel / row-partition exchange executed under RCCL (VERDICT
+r03 #4): a 1-rank "nccl" process group on cuda:0 inside the test process
+(torch.distributed's nccl backend is RCCL on ROCm).  World 1 still takes each
+exchange's group code path — the async all-gathers / all-reduces /
+reduce-scatters, their work.wait() hand-offs onto the caller's stream, the
+CSR side stream waiting on the id all-gathers — so every collective and
+stream hand-off of distributed.py and partition.py runs under RCCL's stream
+semantics once (the multi-rank tests use gloo: RCCL refuses two ranks on one
+device).  Two fused-Adam steps (tail-, then head-batch) against the same
+model trained with no group:
+  * "factors" (distributed.py) and the owner-computes exchange
+    (partition.py "factors", distributed.py "owner"): bit-identical;
+  * "grads" (Σw by torch.sum + all-reduce instead of the kernel's fixed-order
+    sum), the row partition's reduce-scatter ("grads") and query shipping
+    ("queries": the softmax is merged over shards): fp32 rounding, the
+    tolerances of test_dp_grads_gpu / test_partition_gpu / test_ship_gpu."""
+import os
+import socket
+from argparse import Namespace
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+
+from knowledgegraphembedding_amd import KGEAdam, KGEModel, synth
+
+pytestmark = pytest.mark.gpu
+
+E, R, D, B, N, GAMMA, LR = 301, 7, 40, 16, 24, 12.0, 1e-2
+DIMS = {"RotatE": (True, False), "pRotatE": (False, False), "ComplEx": (True, True), "TransE": (False, False),
+        "DistMult": (False, False)}
+DEV = torch.device("cuda", 0)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.fixture(scope="module")
+def rccl_group():
+    torch.cuda.set_device(0)
+    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{_free_port()}", rank=0, world_size=1,
+                            device_id=DEV)
+    try:
+        yield dist.group.WORLD
+    finally:
+        dist.destroy_process_group()
+
+
+def _model(name):
+    torch.manual_seed(0)
+    de, dr = DIMS[name]
+    return KGEModel(name, E, R, D, GAMMA, de, dr).to(DEV)
+
+
+def _batches():
+    out = []
+    for k, mode in enumerate(("tail-batch", "head-batch")):
+        pos, neg, w = synth.kge_batch(80 + k, B, N, E, R)
+        out.append((torch.from_numpy(pos).to(DEV), torch.from_numpy(neg).to(DEV), torch.from_numpy(w).to(DEV), mode))
+    return out
+
+
+def _args(group, reg, uni, exchange=None):
+    return Namespace(cuda=True, negative_adversarial_sampling=not uni, adversarial_temperature=0.8, uni_weight=uni,
+                     regularization=reg, dp_group=group, dp_exchange=exchange)
+
+
+def _train(name, reg, uni, group=None, dp_exchange=None, part_exchange=None):
+    model = _model(name)
+    part = None
+    if part_exchange is not None:
+        from knowledgegraphembedding_amd.partition import EntityRowPartition
+        part = EntityRowPartition(model, group, exchange=part_exchange)
+        params = part.parameters()
+    else:
+        params = [p for p in model.parameters() if p.requires_grad]
+    opt = KGEAdam(params, lr=LR)
+    it = iter(_batches())
+    logs = [dict(KGEModel.train_step(model, opt, it, _args(group, reg, uni, dp_exchange))) for _ in range(2)]
+    torch.cuda.synchronize()
+    ent = (part.materialize() if part is not None and part.exchange == "queries" else model.entity_embedding)
+    return {"logs": logs, "ent": ent.detach().cpu().numpy(), "rel": model.relation_embedding.detach().cpu().numpy(),
+            "mod": model.modulus.detach().cpu().numpy() if name == "pRotatE" else None}
+
+
+def test_group_is_rccl(rccl_group):
+    """The group really is RCCL, and a collective on a device tensor runs."""
+    assert dist.get_backend(rccl_group) == "nccl"
+    assert dist.get_world_size(rccl_group) == 1
+    t = torch.arange(5, dtype=torch.float32, device=DEV)
+    work = dist.all_reduce(t, async_op=True)
+    work.wait()
+    assert torch.equal(t.cpu(), torch.arange(5, dtype=torch.float32))
+    print("RCCL", torch.cuda.nccl.version())
+
+
+@pytest.mark.parametrize("name,reg,uni", [("RotatE", 0.0, False), ("pRotatE", 1e-4, True), ("ComplEx", 1e-4, False)])
+@pytest.mark.parametrize("how", ["factors", "owner", "grads", "rowpart-grads", "queries"])
+def test_exchange_under_rccl(rccl_group, how, name, reg, uni):
+    ref = _train(name, reg, uni)
+    if how == "factors":
+        got = _train(name, reg, uni, rccl_group, dp_exchange="factors")
+    elif how == "owner":
+        got = _train(name, reg, uni, rccl_group, part_exchange="factors")
+    elif how == "grads":
+        got = _train(name, reg, uni, rccl_group, dp_exchange="grads")
+    elif how == "rowpart-grads":
+        got = _train(name, reg, uni, rccl_group, part_exchange="grads")
+    else:
+        got = _train(name, reg, uni, rccl_group, part_exchange="queries")
+    bitwise = how in ("factors", "owner")
+    for k in ("ent", "rel") + (("mod",) if name == "pRotatE" else ()):
+        if bitwise:
+            assert np.array_equal(got[k], ref[k]), (how, k, float(np.abs(got[k] - ref[k]).max()))
+        else:
+            np.testing.assert_allclose(got[k], ref[k], rtol=1e-4, atol=2e-6, err_msg=f"{how} {k}")
+    for lg, lr_ in zip(got["logs"], ref["logs"]):
+        for key in ("positive_sample_loss", "negative_sample_loss", "loss") + (("regularization",) if reg else ()):
+            if bitwise and key in ("positive_sample_loss", "negative_sample_loss"):
+                assert lg[key] == lr_[key], (how, key, lg[key], lr_[key])
+            else:
+                assert abs(lg[key] - lr_[key]) <= 1e-5 * max(1.0, abs(lr_[key])), (how, key, lg[key], lr_[key])

@@ -43,7 +43,8 @@ def test_rank_shard_sampler_partitions_each_epoch():
     assert len(left) > 1  # a different left-over id each epoch (here)
     for n in range(1, 40):
         for world in (2, 3, 4, 8):
-            assert len({len(list(RankShardSampler(n, r, world, 5))) for r in range(world)}) == 1
+            if n >= world:  # (fewer triples than ranks raises: test_fewer_triples_than_ranks_raises)
+                assert len({len(list(RankShardSampler(n, r, world, 5))) for r in range(world)}) == 1
     e0, e1 = list(RankShardSampler(11, 0, 1, 3)), list(RankShardSampler(11, 0, 1, 3))
     assert e0 == e1  # same seed and epoch → same order on every rank
 
@@ -80,3 +81,12 @@ def test_single_process_keeps_reference_loader():
     assert isinstance(it.iterator_head, type(it.iterator_tail))
     p, n, w, mode = next(it)
     assert mode == "tail-batch" and p.shape == (4, 3) and n.shape == (4, 4)
+
+
+def test_fewer_triples_than_ranks_raises():
+    """with fewer training triples than ranks every shard is empty
+    and training would spin on empty batches; the sampler refuses instead."""
+    import pytest
+    with pytest.raises(ValueError, match="cannot be sharded"):
+        RankShardSampler(1, 0, 2, 3)
+    assert len(RankShardSampler(2, 1, 2, 3)) == 1
