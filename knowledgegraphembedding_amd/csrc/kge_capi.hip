@@ -113,6 +113,7 @@ struct Carver {
 struct GradWs {
   float *g, *q, *dq, *ent_contrib, *rel_contrib, *row_stats, *reg_partial, *wsum;
   int32_t *keys, *cnt, *off, *tmp, *occ;
+  int32_t *bkt, *bkt_cnt;  // occurrence buckets [E, BKT_CAP] + counts [E] (the single-call step)
   float* q_sl;  // slice-major q for the sliced entity pass (KGE_ENT_QSL)
   void* scan_tmp;
   size_t scan_tmp_bytes;
@@ -136,6 +137,8 @@ GradWs carve_grad(void* ws, const kge_model_desc* m, int64_t B, int64_t n, size_
   w.tmp = c.take<int32_t>(N);
   w.occ = c.take<int32_t>(N);
   w.q_sl = c.take<float>(8 * B * 512);  // up to 8 slices × B rows × (64 + 64) float4 slots
+  w.bkt = c.take<int32_t>(m->nentity * (int64_t)BKT_CAP);
+  w.bkt_cnt = c.take<int32_t>(m->nentity);
   w.scan_tmp_bytes = csr_scan_temp_bytes(nb);
   w.scan_tmp = c.take<uint8_t>((int64_t)w.scan_tmp_bytes);
   *bytes = c.off + 256;
@@ -309,7 +312,18 @@ int run_grad(const kge_model_desc* m, const Geom& geo, int mode, const int64_t* 
   ra.q_sl = q_slm ? w.q_sl : nullptr;
   ra.q_sl_w = q_slm ? (geo.eg.S + nsl - 1) / nsl : 0;
   const bool rel_side = sd && !rel_fused;
+  // occurrence buckets filled by k_row instead of the CSR (KGE_ENT_BUCKETS,
+  // default on): the single-call step on the slice-major path, when the
+  // average bucket is far below its capacity (an overflowed bucket is still
+  // exact, only slow).  No side stream: no fork marker, no join, nothing
+  // beside k_row.
+  const bool buckets = q_slm && env_int("KGE_ENT_BUCKETS", 1) != 0 &&
+                       (double)B * (double)(n + 2) <= 32.0 * (double)m->nentity;
+  ra.bkt = buckets ? w.bkt : nullptr;
+  ra.bkt_cnt = buckets ? w.bkt_cnt : nullptr;
   RelArgs rl;
+  memset(&rl, 0, sizeof(rl));
+  rl.pos = buckets ? pos : nullptr;
   rl.rel = m->relation_embedding; rl.R = m->nrelation; rl.E = m->nentity; rl.B = B; rl.Bn = B * n; rl.Lr = Lr;
   rl.off = w.off; rl.occ = w.occ; rl.rel_contrib = w.rel_contrib; rl.reg3 = 3.f * reg;
   rl.reg_partial = w.reg_partial + ent_parts; rl.grad_rel = grad_relation;
@@ -337,11 +351,16 @@ int run_grad(const kge_model_desc* m, const Geom& geo, int mode, const int64_t* 
   if (xstage == XS_CSR_ONLY) return launch_status(launch_csr(ca, s));  // kge_train_csr
   if (from_rows) ra.fuse_epi = 0;  // the epilogue reads the gathered dL/dq (k_row_epi)
 
+  const bool use_csr = !csr_ready && !buckets;
   if (phases & KGE_PHASE_ROWS) {
   // fork point: the occurrence CSR needs only the batch indices (recorded
   // before anything else is queued, so the side stream never waits for the
   // row pass)
-  if (sd && !csr_ready) hipEventRecord(sd->fork, s);
+  if (sd && use_csr) hipEventRecord(sd->fork, s);
+  if (buckets) {  // k_row's atomics count from zero
+    const hipError_t me = hipMemsetAsync(w.bkt_cnt, 0, sizeof(int32_t) * (size_t)m->nentity, s);
+    if (me != hipSuccess) return hip_status(me);
+  }
 
   // q build + gather loop on the caller's stream, launched first so the GPU
   // is on the long kernel while the host queues everything else
@@ -351,7 +370,7 @@ int run_grad(const kge_model_desc* m, const Geom& geo, int mode, const int64_t* 
   if (st) return st;
   if (timed) g_timer.mark(s);
 
-  if (!csr_ready) {
+  if (use_csr) {
     if (sd) hipStreamWaitEvent(ss, sd->fork, 0);
     st = launch_status(launch_csr(ca, ss));
     if (st) return st;
@@ -401,7 +420,7 @@ int run_grad(const kge_model_desc* m, const Geom& geo, int mode, const int64_t* 
                          env_int("KGE_FIN_SEPARATE", 0) == 0;
 
   if (phases & KGE_PHASE_ENTITY) {
-  if (sd && !csr_ready)
+  if (sd && use_csr)
     hipStreamWaitEvent(s, sd->csr_done, 0);  // join 1: the entity pass reads the CSR
   if (timed) g_timer.mark(s);
 
@@ -421,6 +440,9 @@ int run_grad(const kge_model_desc* m, const Geom& geo, int mode, const int64_t* 
   ea.adamk = ak;
   ea.align_sl = q_slm ? 0 : entity_slice_align(nsl, geo.eg.S, Le, m->entity_embedding, write_grad ? grad_entity : nullptr, ea.adam);
   ea.q_sl = q_slm ? w.q_sl : nullptr;
+  ea.bkt = buckets ? w.bkt : nullptr;
+  ea.bkt_cnt = buckets ? w.bkt_cnt : nullptr;
+  ea.pos = pos; ea.neg = neg; ea.neg_stride = neg_stride;
   ea.rel = rl;
   ea.B = B;
   ea.rel_blocks = rel_fused ? (m->nrelation + 3) / 4 : 0;

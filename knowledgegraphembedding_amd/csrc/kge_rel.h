@@ -16,7 +16,9 @@ namespace kge {
 // not set by this path)
 template <int U, bool P4 = false>
 __device__ __forceinline__ void rel_row_chunks(const RelArgs& a, int64_t rr, int lane) {
-  const int32_t b0 = a.off[a.E + rr], b1 = a.off[a.E + rr + 1];
+  // a.pos (the single-call step, no CSR): the rows of this relation found by
+  // scanning the batch's relation ids, ascending — the CSR bucket's order
+  const int32_t b0 = a.pos ? 0 : a.off[a.E + rr], b1 = a.pos ? 0 : a.off[a.E + rr + 1];
   const float* row = a.rel + rr * a.Lr;
   const bool v4 = (a.Lr % 4) == 0;
   const int nchunk = v4 ? a.Lr / 4 : a.Lr;  // float4 chunks, or single floats
@@ -28,7 +30,7 @@ __device__ __forceinline__ void rel_row_chunks(const RelArgs& a, int64_t rr, int
 #pragma unroll
       for (int e = 0; e < 4; ++e) acc[u][e] = 0.f;
     int32_t p = b0;
-    if (P4 && v4) {
+    if (P4 && v4 && !a.pos) {
       // four occurrences' rows in flight per iteration (a relation can have
       // thousands of occurrences in a large global batch); the sums keep the
       // ascending occurrence order, so the bits are those of the plain loop
@@ -51,8 +53,26 @@ __device__ __forceinline__ void rel_row_chunks(const RelArgs& a, int64_t rr, int
           }
       }
     }
-    for (; p < b1; ++p) {
-      const int64_t i = a.occ[p] - a.Bn - 2 * a.B;
+    // the occurrences in order: the CSR bucket's, or (a.pos) the rows whose
+    // relation is rr, found 64 batch rows at a time
+    int64_t r0 = 0;
+    uint64_t mask = 0;
+    while (true) {
+      int64_t i;
+      if (!a.pos) {
+        if (p >= b1) break;
+        i = a.occ[p++] - a.Bn - 2 * a.B;
+      } else {
+        while (!mask && r0 < a.B) {
+          const int64_t ii = r0 + lane;
+          mask = __ballot(ii < a.B && a.pos[(ii < a.B ? ii : 0) * 3 + 1] == rr);
+          r0 += 64;
+        }
+        if (!mask) break;
+        const int b = __builtin_ctzll(mask);
+        mask &= mask - 1;
+        i = r0 - 64 + b;
+      }
       const float* src = a.rel_contrib + i * a.Lr;
 #pragma unroll
       for (int u = 0; u < U; ++u) {

@@ -1,16 +1,18 @@
 """BASELINE config 4 at its own shape (best_config.sh:4: RotatE FB15k-237,
 E = 14541, R = 237, d = 1000 -de, γ = 9, b = 1024 per rank, n = 256, -adv):
-the data-parallel exchanges run on cuda:0 with 2 and 4 ranks (gloo; the
+the data-parallel exchanges run on cuda:0 with 2, 4 and 8 ranks (gloo; the
 driver's 8-GPU runs use RCCL) for two fused-Adam steps (tail-, then head-
 batch) and must equal ONE process training on the global batch of
-world × 1024 rows bit for bit:
+world × 1024 rows bit for bit — at world 8 that is config 4's own global
+batch of 8192 rows with the exchange `auto` picks there:
 
   * "owner" (forced at world 2 and 4): the row factors all-gathered, each rank's
     entity pass + fused Adam over its 1/N of the rows in OWNER_CHUNKS chunks,
     the chunks' rows all-gathered behind the next chunk's pass
     (partition.EntityRowPartition exchange "factors"; 14541 rows = 7271 + 7270
-    at world 2, 3636 ×3 + 3633 at world 4, so the chunked all-gather, its
-    slice rule and the owner's CSR range run at the real row counts);
+    at world 2, 3636 ×3 + 3633 at world 4, 1818 ×7 + 1815 at world 8, so the
+    chunked all-gather, its slice rule and the owner's CSR range run at the
+    real row counts);
   * "factors" (the world-2 default): the factors all-gathered, the global
     entity pass on every rank.
 
@@ -106,7 +108,7 @@ def _worker(rank, world, port, exchange, out):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,exchange", [(2, "owner"), (4, "owner"), (2, "factors")])
+@pytest.mark.parametrize("world,exchange", [(2, "owner"), (4, "owner"), (8, "owner"), (2, "factors")])
 def test_config4_shape_matches_one_process(world, exchange):
     out = mp.Manager().dict()
     spawn_ranks(_worker, (world, _free_port(), exchange, out), world)

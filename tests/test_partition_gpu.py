@@ -97,48 +97,67 @@ def _yago_model():
     return KGEModel("RotatE", YE, YR, YD, 24.0, True, False).to("cuda:0")
 
 
-def _yago_batches(dev):
+def _yago_batches(dev, world=1):
+    """The global batches of the two steps: world × 1024 rows (rank order)."""
     out = []
     for k, mode in enumerate(("tail-batch", "head-batch")):
-        pos, neg, w = synth.kge_batch(95 + k, YB, YN, YE, YR)
+        pos, neg, w = synth.kge_batch(95 + k, world * YB, YN, YE, YR)
         out.append((torch.from_numpy(pos).to(dev), torch.from_numpy(neg).to(dev), torch.from_numpy(w).to(dev), mode))
     return out
 
 
-def _yago_worker(rank, world, port, out):
+ROWS8 = [0, 1, 100, 511, 512, 700, 900, 1023]
+
+
+def _yago_worker(rank, world, port, exchange, out):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     torch.cuda.set_device(0)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from knowledgegraphembedding_amd.partition import EntityRowPartition
     model = _yago_model()
-    part = EntityRowPartition(model)
+    part = EntityRowPartition(model, dist.group.WORLD, exchange=exchange)
     opt = KGEAdam(part.parameters(), lr=1e-4)
-    sl = slice(rank * YB // world, (rank + 1) * YB // world)
-    it = iter([(p[sl], n[sl], w[sl], m) for p, n, w, m in _yago_batches("cuda:0")])
+    sl = slice(rank * YB, (rank + 1) * YB)
+    it = iter([(p[sl], n[sl], w[sl], m) for p, n, w, m in _yago_batches("cuda:0", world)])
     logs = [dict(KGEModel.train_step(model, opt, it, _args(dist.group.WORLD))) for _ in range(2)]
     torch.cuda.synchronize()
-    out[rank] = {"logs": logs, "ent": model.entity_embedding.detach()[torch.from_numpy(SAMPLE_ROWS).cuda()].cpu().numpy(),
-                 "rel": model.relation_embedding.detach().cpu().numpy()}
+    ent = part.materialize()  # query shipping: the shards gathered (collective); otherwise the replica
+    res = {"logs": logs, "ent": ent.detach()[torch.from_numpy(SAMPLE_ROWS).cuda()].cpu().numpy(),
+           "rel": model.relation_embedding.detach().cpu().numpy()}
+    if rank == 0:
+        # 8 rows' scores of the trained (gathered) table against the oracle's op chain on the same table
+        from oracle import kge_oracle as O
+        pos, neg, _, _ = _yago_batches("cpu", world)[0]
+        P, N = pos[ROWS8], neg[ROWS8]
+        with torch.no_grad():
+            s = model((P.cuda(), N.cuda()), "tail-batch").cpu().numpy()
+        sref = O.forward("RotatE", ent.detach().cpu(), model.relation_embedding.detach().cpu(), None, (P, N),
+                         "tail-batch", 24.0, model.embedding_range.item()).numpy()
+        res["score_err"] = float(np.max(np.abs(s - sref) / np.maximum(np.abs(sref), 1.0)))
+    out[rank] = res
     dist.destroy_process_group()
 
 
-def test_row_partition_yago3_10_shape():
+@pytest.mark.parametrize("world,exchange", [(2, "grads"), (2, "factors"), (2, "queries"), (4, "queries")])
+def test_row_partition_yago3_10_shape(world, exchange):
     """BASELINE config 5's shape (RotatE, E = 123182, d = 1000 -de, n = 1024;
-    985 MB entity table): 2 ranks owning half of the rows each, 512 positives
-    per rank, two KGEAdam steps, against one process training the 1024-row
-    global batch — sampled entity rows, the relation table and the losses to
-    fp32 rounding.  Then 8 rows' scores on the trained table against the CPU
-    oracle's forward."""
-    from oracle import kge_oracle as O
-    world = 2
+    985 MB entity table) at its own 1024 positives per rank:
+    `world` ranks each owning 1/world of the rows — the reduce-scatter
+    ("grads"), owner-computes ("factors", run.py's default) and query-shipping
+    ("queries": no rank holds the table; q vectors travel) exchanges — for two
+    KGEAdam steps, against one process training the world × 1024-row global
+    batch: sampled entity rows, the relation table and the losses to fp32
+    rounding.  Then rank 0's trained (gathered) table scores 8 rows against the
+    CPU oracle's op chain on that same table (north-star tolerance)."""
     out = mp.Manager().dict()
-    spawn_ranks(_yago_worker, (world, _free_port(), out), world)
+    spawn_ranks(_yago_worker, (world, _free_port(), exchange, out), world)
     model = _yago_model()
     opt = KGEAdam([p for p in model.parameters() if p.requires_grad], lr=1e-4)
-    it = iter(_yago_batches("cuda:0"))
+    it = iter(_yago_batches("cuda:0", world))
     ref = [dict(KGEModel.train_step(model, opt, it, _args(None))) for _ in range(2)]
     ent = model.entity_embedding.detach()[torch.from_numpy(SAMPLE_ROWS).cuda()].cpu().numpy()
     rel = model.relation_embedding.detach().cpu().numpy()
+
     def close(got, want, what):
         # an element whose gradient sums to ~0 can take Adam's ±lr step with
         # the other sign when the two paths round the sum differently: allow
@@ -149,18 +168,9 @@ def test_row_partition_yago3_10_shape():
 
     for rank in range(world):
         r = out[rank]
-        close(r["ent"], ent, "entity rows")
-        close(r["rel"], rel, "relation table")
+        close(r["ent"], ent, ("entity rows", rank))
+        close(r["rel"], rel, ("relation table", rank))
         for got, want in zip(r["logs"], ref):
             for k in ("positive_sample_loss", "negative_sample_loss", "loss"):
                 np.testing.assert_allclose(got[k], want[k], rtol=2e-5)
-    # scores of 8 rows on the trained table vs the oracle (north-star tolerance)
-    pos, neg, _ = _yago_batches("cpu")[0][:3]
-    rows = [0, 1, 100, 511, 512, 700, 900, 1023]
-    P, N = pos[rows], neg[rows]
-    with torch.no_grad():
-        s = model((P.cuda(), N.cuda()), "tail-batch").cpu().numpy()
-    erange = model.embedding_range.item()
-    sref = O.forward("RotatE", model.entity_embedding.detach().cpu(), model.relation_embedding.detach().cpu(), None,
-                     (P, N), "tail-batch", 24.0, erange).numpy()
-    assert np.all(np.abs(s - sref) <= 1e-4 * np.maximum(np.abs(sref), 1.0))
+    assert out[0]["score_err"] <= 1e-4, out[0]["score_err"]
