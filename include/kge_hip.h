@@ -77,6 +77,9 @@ enum kge_status {
  *                     its queries' rotation from these values, so its ranks are the reference's
  *                     bit for bit; NULL = correctly rounded cos / sin on the device.  Training
  *                     and kge_score do not read it (scores are held to 1e-4, not to bits).
+ *                     "The reference" is its CPU run: with --cuda its test_step evaluates
+ *                     cos / sin and sum(dim=2) with ATen's GPU kernels, whose bits are not
+ *                     reproduced here (parity against that configuration is unpinned).
  */
 typedef struct kge_model_desc {
     int32_t model;
@@ -484,7 +487,10 @@ int kge_rank_finish_sin(const kge_model_desc *m, int32_t mode, int64_t nq, const
  *   command 0: disable and reset;
  *   command 2: synchronise the recorded events and write the summed
  *              milliseconds per stage to stage_ms_out[0..5] and the number of
- *              timed calls to stage_ms_out[6] (n_out >= 7).
+ *              timed calls to stage_ms_out[6] (n_out >= 7);
+ *   command 3: the same per timed call: stage_ms_out[7c .. 7c+5] the call's
+ *              stage times, stage_ms_out[7c+6] its start (ms after the first
+ *              timed call's start); n_out >= 7 × timed calls.
  * Not graph-capturable while enabled.
  */
 #define KGE_TIMER_STAGES 6

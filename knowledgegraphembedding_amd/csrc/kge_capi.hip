@@ -1072,7 +1072,7 @@ int rank_impl(const kge_model_desc* m, int32_t mode, const int64_t* queries, int
   ra.lib_sin = (stage != RS_ALL) ? 1 : 0;
   // the split-bf16 tile's error bound in units of u·‖q‖·max‖e‖ (kge_rank_mfma.hip)
   const int64_t xns = xsplit_nslab(m->entity_dim);
-  ra.fast_u = (rp == RP_MFMA) ? (float)(546.0 + 1.02 * xns + 0.05 * xns * 16) : 0.f;
+  ra.fast_u = (rp == RP_MFMA) ? (float)(546.0 + 1.02 * xns + 0.05 * xns * 16 + (xsplit_lolo() ? 0.0 : 64.2)) : 0.f;
   if (stage == RS_ARGS) return launch_status(ops.rank_ref(mode, 3, ra, s));
   EmitArgs ea;
   ea.gt = w.gt; ea.eq = w.eq; ea.gtx = w.gtx; ea.eqx = w.eqx; ea.ucnt = w.ucnt; ea.true_id = w.true_id;
@@ -1187,9 +1187,30 @@ int kge_stage_timer(int32_t command, float* stage_ms_out, int32_t n_out) {
     g_timer.period = (command == 1 && n_out > 0) ? n_out : 1;
     return KGE_OK;
   }
+  const size_t calls = g_timer.used / NS_;
+  if (command == 3) {
+    // per timed call: the 6 stage times, then the call's start relative to the
+    // first timed call's start (ms, device clock)
+    if (!stage_ms_out || (size_t)n_out < calls * NS_) return KGE_ERR_ARG;
+    for (size_t c = 0; c < calls; ++c) {
+      hipEvent_t* e = &g_timer.ev[c * NS_];
+      hipError_t err = hipEventSynchronize(e[NS_ - 1]);
+      if (err != hipSuccess) return hip_status(err);
+      for (int k = 0; k < KGE_TIMER_STAGES; ++k) {
+        float ms = 0.f;
+        err = hipEventElapsedTime(&ms, e[k], e[k + 1]);
+        if (err != hipSuccess) return hip_status(err);
+        stage_ms_out[c * NS_ + k] = ms;
+      }
+      float t0 = 0.f;
+      err = hipEventElapsedTime(&t0, g_timer.ev[0], e[0]);
+      if (err != hipSuccess) return hip_status(err);
+      stage_ms_out[c * NS_ + KGE_TIMER_STAGES] = t0;
+    }
+    return KGE_OK;
+  }
   if (command != 2 || !stage_ms_out || n_out < NS_) return KGE_ERR_ARG;
   for (int k = 0; k < NS_; ++k) stage_ms_out[k] = 0.f;
-  const size_t calls = g_timer.used / NS_;
   for (size_t c = 0; c < calls; ++c) {
     hipEvent_t* e = &g_timer.ev[c * NS_];
     hipError_t err = hipEventSynchronize(e[NS_ - 1]);

@@ -384,7 +384,7 @@ struct XArgs {
 // wn18rr's 25 query tiles: 2.2 GB per launch, 43 % MFMA-busy).  The order is
 // a speed property only.  Returns false for the grid's idle tail blocks.
 __device__ __forceinline__ bool xcd_tile(const XArgs& a, int& x, int& y) {
-  const int b = blockIdx.x, k = b & 7, i = b >> 3;
+  const int b = blockIdx.x, k = b & 7, i = b >> 3;  // (1-D grid)
   const int nxk = (a.gx - k + 7) >> 3;  // candidate tiles of XCD k
   if (i >= nxk * a.gy) return false;
   const int per = a.group * a.gy;
@@ -403,16 +403,25 @@ __device__ __forceinline__ bool xcd_tile(const XArgs& a, int& x, int& y) {
 // measured equal (530 vs 523 µs, profiles/r03/rank/ab_tile_variants.txt).
 // (Timing diagnostics that dropped the MFMAs, the LDS-DMA or the epilogue —
 // measurements in profiles/r03/rank/ab_tile_variants.txt — are not in the tree.)
-template <int TQ>
+// WM = waves along the candidates: 2 (128 candidates per workgroup, 256
+// threads, 2 workgroups per CU) or 4 (256 candidates, 512 threads, one
+// workgroup per CU: the same 64×64 per wave, a third less L2 → LDS traffic
+// per MFMA — each slab's query piece feeds twice the candidates).
+template <int TQ, int WM = 2>
 struct XTile {
   static constexpr int BQ = 64 * TQ;                   // queries per workgroup
-  static constexpr int STAGE = (8 + 4 * TQ) * 512;     // bf16 per ring stage: E hi|lo (4 KB each), Q hi|lo (2·TQ KB each)
-  static constexpr int CPW = 2 + TQ;                   // 1 KB DMA chunks per wave per slab
+  static constexpr int BNX = 64 * WM;                  // candidates per workgroup
+  static constexpr int NT = 128 * WM;                  // threads
+  // bf16 per ring stage: per 128-candidate block E hi | lo (4 KB each), then Q hi | lo (2·TQ KB each)
+  static constexpr int STAGE = (4 * WM + 4 * TQ) * 512;
+  static constexpr int CPW = (4 * WM + 4 * TQ) / (2 * WM);  // 1 KB DMA chunks per wave per slab
+  static_assert((4 * WM + 4 * TQ) % (2 * WM) == 0, "DMA chunks must split evenly over the waves");
 };
 
-template <bool GATHER, int TQ>
-__global__ __launch_bounds__(256, TQ == 1 ? 3 : 2) void k_rank_mfma_x(XArgs a) {
-  using X = XTile<TQ>;
+template <bool GATHER, int TQ, int WM = 2, bool LL = true>
+__global__ __launch_bounds__(128 * WM, WM == 4 ? 1 : (TQ == 1 ? 3 : 2)) void k_rank_mfma_x(XArgs a) {
+  using X = XTile<TQ, WM>;
+  static_assert(!GATHER || WM == 2, "the gather pass uses 128-row candidate tiles");
   // one LDS array: [XS_NST stages][E_hi | E_lo | Q_hi | Q_lo] then arow/brow, sts, sdl, cgt
   __shared__ __attribute__((aligned(16))) uint16_t smem[XS_NST * X::STAGE + 128 * 4 * 2 + 128 * 2 * 2 + 128 * 2 * 3];
   int64_t* arow = reinterpret_cast<int64_t*>(smem + XS_NST * X::STAGE);
@@ -425,7 +434,7 @@ __global__ __launch_bounds__(256, TQ == 1 ? 3 : 2) void k_rank_mfma_x(XArgs a) {
   int tx = 0, ty = (int)blockIdx.y;
   if (!GATHER && !xcd_tile(a, tx, ty)) return;  // (block-uniform)
   const int64_t q0 = (int64_t)ty * X::BQ;
-  const int64_t e0 = (int64_t)tx * BN;
+  const int64_t e0 = (int64_t)tx * X::BNX;
   if (t < 128) {
     const int64_t q = q0 + t;
     const bool in = t < X::BQ && q < a.nq;
@@ -444,14 +453,14 @@ __global__ __launch_bounds__(256, TQ == 1 ? 3 : 2) void k_rank_mfma_x(XArgs a) {
   const auto rq = buf_rsrc(a.qs, a.qs_bytes);
   const auto re = buf_rsrc(a.es, a.es_bytes);
   const int nslab = a.nslab;
-  // 1 KB chunk c of a stage (LDS bytes c·1024 …): c < 8 candidate pieces
-  // (hi: 0-3, lo: 4-7; 32 rows each), then the query pieces (hi, lo: 2·TQ
-  // chunks each).  Wave w moves chunks CPW·w … CPW·w + CPW − 1.
+  // 1 KB chunk c of a stage (LDS bytes c·1024 …): c < 4·WM candidate pieces
+  // (per 128-row block: hi 0-3, lo 4-7; 32 rows each), then the query pieces
+  // (hi, lo: 2·TQ chunks each).  Wave w moves chunks CPW·w … CPW·w + CPW − 1.
   int64_t grow[X::CPW];  // GATHER: this lane's source row of each candidate chunk
 #pragma unroll
   for (int k = 0; k < X::CPW; ++k) {
     const int c = X::CPW * w + k;
-    grow[k] = (GATHER && c < 8) ? brow[(c & 3) * 32 + (lane >> 1)] : 0;
+    grow[k] = (GATHER && c < 4 * WM) ? brow[(c & 3) * 32 + (lane >> 1)] : 0;
   }
   const int64_t qrb = (int64_t)ty * X::BQ / 128;           // the queries' 128-row block in the split layout
   const uint32_t qsub = (uint32_t)((ty * X::BQ) & 127) * 32;  // … and their byte offset inside it
@@ -461,19 +470,20 @@ __global__ __launch_bounds__(256, TQ == 1 ? 3 : 2) void k_rank_mfma_x(XArgs a) {
     for (int k = 0; k < X::CPW; ++k) {
       const int c = X::CPW * w + k;
       uint32_t off;
-      const bool cand = c < 8;
+      const bool cand = c < 4 * WM;
       if (cand) {
-        const int piece = c >> 2, sub = c & 3;
+        const int rb = c >> 3, piece = (c >> 2) & 1, sub = c & 3;
         if (GATHER) {
           const int64_t r = grow[k];
           off = (r >= 0) ? (uint32_t)((((r >> 7) * nslab + sl) * 2 + piece) * (2 * XS_PIECE) + (r & 127) * 32 +
                                       (lane & 1) * 16)
                          : XS_OOB;
         } else {
-          off = (uint32_t)((((int64_t)tx * nslab + sl) * 2 + piece) * (2 * XS_PIECE) + sub * 1024 + lane * 16);
+          off = (uint32_t)(((((int64_t)tx * (WM / 2) + rb) * nslab + sl) * 2 + piece) * (2 * XS_PIECE) +
+                           sub * 1024 + lane * 16);
         }
       } else {
-        const int cc = c - 8, piece = cc / (2 * TQ), sub = cc % (2 * TQ);
+        const int cc = c - 4 * WM, piece = cc / (2 * TQ), sub = cc % (2 * TQ);
         off = (uint32_t)(((qrb * nslab + sl) * 2 + piece) * (2 * XS_PIECE) + qsub + sub * 1024 + lane * 16);
       }
       __builtin_amdgcn_raw_ptr_buffer_load_lds(cand ? re : rq,
@@ -483,6 +493,7 @@ __global__ __launch_bounds__(256, TQ == 1 ? 3 : 2) void k_rank_mfma_x(XArgs a) {
   };
   // DMAs issued after slab sl's, when sl is waited for: those of the next
   // min(XS_NST − 2, nslab − 1 − sl) slabs, CPW instructions each (vmcnt counts in order)
+  static_assert(X::CPW == 3 || X::CPW == 4, "vmcnt immediates below");
   auto wait_slab = [&](int sl) {
     const int after = nslab - 1 - sl;
     if (after >= 2) {
@@ -532,16 +543,16 @@ __global__ __launch_bounds__(256, TQ == 1 ? 3 : 2) void k_rank_mfma_x(XArgs a) {
                                    // vmcnt above covers the DMA, __syncthreads' would be vmcnt(0))
     if (sl + XS_NST - 1 < nslab) issue(sl + XS_NST - 1, (sl + XS_NST - 1) % XS_NST);
     if (!live) continue;
-    const uint16_t* Eh = smem + (sl % XS_NST) * X::STAGE;
-    const uint16_t* El = Eh + XS_PIECE;
-    const uint16_t* Qh = Eh + 2 * XS_PIECE;
+    const uint16_t* Es = smem + (sl % XS_NST) * X::STAGE;
+    const uint16_t* Qh = Es + WM * XS_PIECE;
     const uint16_t* Ql = Qh + TQ * 1024;
     bf16x8 eh[2], el[2], qh[TQ], ql[TQ];
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int row = wm * 64 + i * 32 + li;
-      eh[i] = *reinterpret_cast<const bf16x8*>(Eh + row * XS_BK + kh * 8);
-      el[i] = *reinterpret_cast<const bf16x8*>(El + row * XS_BK + kh * 8);
+      const uint16_t* Eh = Es + (row >> 7) * 2 * XS_PIECE;  // this row's 128-row block: hi, then lo
+      eh[i] = *reinterpret_cast<const bf16x8*>(Eh + (row & 127) * XS_BK + kh * 8);
+      el[i] = *reinterpret_cast<const bf16x8*>(Eh + XS_PIECE + (row & 127) * XS_BK + kh * 8);
     }
 #pragma unroll
     for (int j = 0; j < TQ; ++j) {
@@ -567,7 +578,7 @@ __global__ __launch_bounds__(256, TQ == 1 ? 3 : 2) void k_rank_mfma_x(XArgs a) {
         mprev[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(eh[i], qh[j], zero, 0, 0, 0);
         cor[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(eh[i], ql[j], cor[i][j], 0, 0, 0);
         cor[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(el[i], qh[j], cor[i][j], 0, 0, 0);
-        cor[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(el[i], ql[j], cor[i][j], 0, 0, 0);
+        if constexpr (LL) cor[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(el[i], ql[j], cor[i][j], 0, 0, 0);
       }
   }
   f32x16 acc[2][TQ];
@@ -673,6 +684,10 @@ int launch_rank_mfma(int gather, const float* q, const float* ent, int64_t nq, i
 
 // split-bf16 tile: buffer sizes and launchers (path "mfma")
 int64_t xsplit_nslab(int K) { return (K + XS_BK - 1) / XS_BK; }
+bool xsplit_lolo() {
+  const char* e = getenv("KGE_XTILE_LOLO");
+  return !(e && atoi(e) == 0);
+}
 int64_t xsplit_elems(int64_t rows, int K) { return ((rows + 127) / 128) * 128 * xsplit_nslab(K) * XS_BK * 2; }
 
 int launch_split_bf16(const float* src, int64_t rows, int K, uint16_t* dst, hipStream_t s, const int64_t* skip) {
@@ -702,14 +717,32 @@ int launch_rank_mfma_x(int gather, const uint16_t* qs, const uint16_t* es, int64
   const int64_t tile_bytes = (int64_t)BN * a.nslab * XS_BK * 4;
   a.group = (int)std::max<int64_t>(1, (2 << 20) / tile_bytes);
   if (const char* gg = getenv("KGE_XTILE_GROUP")) a.group = std::max(1, atoi(gg));
+  const bool ll = xsplit_lolo();
   if (gather) {
-    if (tq == 2) hipLaunchKernelGGL((k_rank_mfma_x<true, 2>), dim3(1, gy), dim3(256), 0, s, a);
-    else hipLaunchKernelGGL((k_rank_mfma_x<true, 1>), dim3(1, gy), dim3(256), 0, s, a);
+    if (tq == 2) {
+      if (ll) hipLaunchKernelGGL((k_rank_mfma_x<true, 2>), dim3(1, gy), dim3(256), 0, s, a);
+      else hipLaunchKernelGGL((k_rank_mfma_x<true, 2, 2, false>), dim3(1, gy), dim3(256), 0, s, a);
+    } else {
+      hipLaunchKernelGGL((k_rank_mfma_x<true, 1>), dim3(1, gy), dim3(256), 0, s, a);
+    }
     return (int)hipGetLastError();
+  }
+  // KGE_XTILE_WM=4: 256-candidate tiles, one 8-wave workgroup per CU (TQ = 2)
+  const char* wm_env = getenv("KGE_XTILE_WM");
+  const int wmv = (tq == 2 && wm_env && atoi(wm_env) == 4) ? 4 : 2;
+  if (wmv == 4) {
+    a.gx = (int)((E + 255) / 256);
+    a.group = (int)std::max<int64_t>(1, (2 << 20) / (2 * tile_bytes));
+    if (const char* gg = getenv("KGE_XTILE_GROUP")) a.group = std::max(1, atoi(gg));
   }
   const int64_t per_xcd = (int64_t)((a.gx + 7) / 8) * a.gy;  // XCD 0 has the most candidate tiles
   const dim3 gs((unsigned)(8 * per_xcd));
-  if (tq == 1)
+  if (wmv == 4) {
+    if (ll) hipLaunchKernelGGL((k_rank_mfma_x<false, 2, 4>), gs, dim3(512), 0, s, a);
+    else hipLaunchKernelGGL((k_rank_mfma_x<false, 2, 4, false>), gs, dim3(512), 0, s, a);
+  } else if (!ll && tq == 2)
+    hipLaunchKernelGGL((k_rank_mfma_x<false, 2, 2, false>), gs, dim3(256), 0, s, a);
+  else if (tq == 1)
     hipLaunchKernelGGL((k_rank_mfma_x<false, 1>), gs, dim3(256), 0, s, a);
   else
     hipLaunchKernelGGL((k_rank_mfma_x<false, 2>), gs, dim3(256), 0, s, a);

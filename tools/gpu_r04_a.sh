@@ -7,3 +7,4 @@ timeout -k 10 200 python -u bench.py --steps 100 --warmup 10 --no-cpu-baseline -
 KGE_ENT_BUCKETS=0 timeout -k 10 200 python -u bench.py --steps 100 --warmup 10 --no-cpu-baseline --no-rank > gpurun_out/r04_bench_csr.json 2>> gpurun_out/r04_bench_buckets.err || exit $?
 timeout -k 10 200 python -u bench.py --steps 100 --warmup 10 --no-cpu-baseline --no-rank > gpurun_out/r04_bench_buckets2.json 2>> gpurun_out/r04_bench_buckets.err || exit $?
 timeout -k 10 400 python -u -m pytest tests/test_dp_config4_gpu.py tests/test_partition_gpu.py -x -v -s --timeout 300 --timeout-method thread > gpurun_out/r04_dp.log 2>&1 || exit $?
+timeout -k 10 120 python -u tools/hump_trace.py --steps 150 --warmup 5 > gpurun_out/r04_hump.jsonl 2> gpurun_out/r04_hump.err || exit $?
