@@ -684,9 +684,9 @@ int launch_rank_mfma(int gather, const float* q, const float* ent, int64_t nq, i
 
 // split-bf16 tile: buffer sizes and launchers (path "mfma")
 int64_t xsplit_nslab(int K) { return (K + XS_BK - 1) / XS_BK; }
-bool xsplit_lolo() {
+bool xsplit_lolo() {  // default: dropped (9 % faster tile, profiles/r04/rank/ab_tile_wm_lolo.txt)
   const char* e = getenv("KGE_XTILE_LOLO");
-  return !(e && atoi(e) == 0);
+  return e && atoi(e) == 1;
 }
 int64_t xsplit_elems(int64_t rows, int K) { return ((rows + 127) / 128) * 128 * xsplit_nslab(K) * XS_BK * 2; }
 

@@ -49,8 +49,8 @@ pytestmark = pytest.mark.gpu
 DEV = torch.device("cuda", 0)
 U = 2.0 ** -24
 EXACT = ("TransE", "DistMult", "ComplEx", "RotatE", "pRotatE")
-PATHS = {"DistMult": ("auto", "auto/wm4", "mfma32", "tile", "scan"),
-         "ComplEx": ("auto", "auto/wm4", "mfma32", "tile", "scan"),
+PATHS = {"DistMult": ("auto", "auto/lolo", "mfma32", "tile", "scan"),
+         "ComplEx": ("auto", "auto/lolo", "mfma32", "tile", "scan"),
          "TransE": ("auto", "scan"), "RotatE": ("auto", "scan"), "pRotatE": ("auto", "scan")}
 
 
@@ -125,10 +125,10 @@ def run_case(tag, name, E, R, d, gamma, seed, queries, filters, refs, report):
         base = None
         for path in PATHS[name]:
             import os
-            os.environ["KGE_XTILE_WM"] = "4" if path.endswith("/wm4") else "2"
+            os.environ["KGE_XTILE_LOLO"] = "1" if path.endswith("/lolo") else "0"
             ranks, ties, listed = m.rank_queries(qs, filters, mode, path=path.split("/")[0], listed=True,
                                                  relation_trig=trig)
-            os.environ.pop("KGE_XTILE_WM", None)
+            os.environ.pop("KGE_XTILE_LOLO", None)
             if base is None:
                 base = (ranks, ties)
             else:
@@ -268,7 +268,7 @@ def test_host_sin_matches_reference(golden_info, g_full, capsys):
     assert differ == 0.0, "this host's sin differs from the reference's: pRotatE ranks would follow this host's"
 
 
-@pytest.mark.parametrize("wm", ["2", "4", "4/nolo"])
+@pytest.mark.parametrize("wm", ["2", "2/lolo", "4"])
 @pytest.mark.parametrize("name,E,d", [("DistMult", 300, 50), ("DistMult", 257, 37), ("DistMult", 1000, 130),
                                       ("ComplEx", 300, 25), ("ComplEx", 513, 33), ("DistMult", 129, 16)])
 def test_split_bf16_tile_matches_other_paths(name, E, d, wm, monkeypatch):
@@ -281,10 +281,10 @@ def test_split_bf16_tile_matches_other_paths(name, E, d, wm, monkeypatch):
     wm = 4: the 256-candidate tile (KGE_XTILE_WM=4, one 8-wave workgroup per
     CU), whose candidate tiles span two 128-row blocks of the split layout
     (E = 129, 257, 300, 513: a last tile with one block past the table);
-    "nolo": without the lo·lo products (KGE_XTILE_LOLO=0, the window widened
-    by their bound)."""
+    "lolo": with the lo·lo products (KGE_XTILE_LOLO=1; by default they are
+    dropped and the window widened by their bound)."""
     monkeypatch.setenv("KGE_XTILE_WM", wm.split("/")[0])
-    monkeypatch.setenv("KGE_XTILE_LOLO", "0" if wm.endswith("nolo") else "1")
+    monkeypatch.setenv("KGE_XTILE_LOLO", "1" if wm.endswith("lolo") else "0")
     R = 7
     m, ent, rel, _, _ = build(name, E, R, d, 12.0, 17)
     with torch.no_grad():
@@ -307,14 +307,15 @@ def test_split_bf16_tile_matches_other_paths(name, E, d, wm, monkeypatch):
             assert np.array_equal(r, r0) and np.array_equal(t, t0), (name, E, d, mode, p)
 
 
-@pytest.mark.parametrize("wm", ["2", "4"])
+@pytest.mark.parametrize("wm", ["2", "2/lolo", "4"])
 @pytest.mark.parametrize("name", ["DistMult", "ComplEx"])
 def test_split_bf16_tile_wide_dynamic_range(name, wm, monkeypatch):
     """The split tile's error bound is rigorous, not statistical: entity and
     relation values spread over 10^-30 … 10^3 (bf16 lo pieces and products
     that underflow, rows that differ by 30 orders of magnitude, exact zeros)
     must still give the wave scan's ranks and ties."""
-    monkeypatch.setenv("KGE_XTILE_WM", wm)
+    monkeypatch.setenv("KGE_XTILE_WM", wm.split("/")[0])
+    monkeypatch.setenv("KGE_XTILE_LOLO", "1" if wm.endswith("lolo") else "0")
     E, R, d = 500, 5, 48
     m, ent, rel, _, _ = build(name, E, R, d, 12.0, 23)
     g = np.random.default_rng(11)

@@ -51,6 +51,8 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--path", default="auto", choices=("auto", "mfma", "mfma32", "tile", "scan"))
     ap.add_argument("--cpu-sample", type=int, default=0, help="queries timed through the CPU oracle (0: skip)")
+    ap.add_argument("--rank-trig", default="reference", choices=("reference", "device"),
+                    help="RotatE / pRotatE: the reference's host trig (exact ranks) or device trig")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     h = synth.randint(901, (NTRUE,), E)
@@ -64,14 +66,15 @@ def main():
         de, dr = DIMS[name]
         torch.manual_seed(0)
         m = KGEModel(name, E, R, a.hidden_dim, 12.0, de, dr).to(dev)
+        m.rank_trig = a.rank_trig
         K = m.entity_dim
         times = []
         ranks = None
         for rep in range(a.reps + 1):
             torch.cuda.synchronize()
             t0 = time.perf_counter()
-            rh, _ = m.rank_queries(test, index, "head-batch", path=a.path)
-            rt, _ = m.rank_queries(test, index, "tail-batch", path=a.path)
+            rh, _, lh = m.rank_queries(test, index, "head-batch", path=a.path, listed=True)
+            rt, _, lt = m.rank_queries(test, index, "tail-batch", path=a.path, listed=True)
             torch.cuda.synchronize()
             if rep:
                 times.append(time.perf_counter() - t0)
@@ -82,9 +85,10 @@ def main():
         res = {"model": name, "hidden_dim": a.hidden_dim, "entity_dim": K, "queries": nq,
                "seconds": dt, "queries_per_s": nq / dt, "candidate_scores_per_s": nq * E / dt,
                "tflops": flops / dt / 1e12,
-               "path": rank_path(name, K, a.path),
+               "path": rank_path(name, K, a.path), "rank_trig": a.rank_trig,
                "pair_terms_per_s": nq * E * (K // 2 if name in ("RotatE", "ComplEx") else K) / dt,
-               "mrr": float(np.mean(1.0 / ranks))}
+               "mrr": float(np.mean(1.0 / ranks)),
+               "listed_per_query": float(np.mean(np.concatenate([lh, lt])))}
         if res["path"].startswith("mfma"):
             res["roofline"] = {"bound": "mfma", "achieved": res["tflops"], "peak": FP32_PEAK_TF, "unit": "TFLOP/s",
                                "frac": res["tflops"] / FP32_PEAK_TF}
