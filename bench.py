@@ -221,7 +221,8 @@ def rank_section(dev, reps: int = 3) -> dict:
     wn18rr-shape test triples in both directions (6268 queries, E=40943, d=500)
     against a synthetic filter graph of wn18rr's 93,003 true triples
     (tools/bench_rank.py, same data).  The tile computes each fp32 product as
-    four bf16 MFMA products (x = x_hi + x_lo): `frac` = the bf16 flops the
+    three bf16 MFMA products (x = x_hi + x_lo; the lo·lo product dropped,
+    inside the window's bound): `frac` = the bf16 flops the
     matrix cores issue (tile padding included) / wall time of the whole pass
     (host CSR, bitmap, operand split, window, MFMA tile, refinement,
     read-back) / the 2.5 PF bf16 dense spec; `fp32_equivalent_tflops` =
@@ -250,17 +251,20 @@ def rank_section(dev, reps: int = 3) -> dict:
             if rep and (best is None or dt < best):
                 best = dt
         flops = 2.0 * 2 * ntest * Ew * K  # fp32 products the ranking needs (both directions)
-        # what the matrix cores issue: four bf16 products per fp32 product over
-        # the tile-padded shape (128-query and 128-candidate tiles, 16-k slabs)
+        # what the matrix cores issue: three bf16 products per fp32 product (hi·hi,
+        # hi·lo, lo·hi; four with KGE_XTILE_LOLO=1) over the tile-padded shape
+        # (128-query and 128-candidate tiles, 16-k slabs)
         pad = lambda x, m: -(-x // m) * m  # noqa: E731
-        issued = 2.0 * 4 * 2 * pad(ntest, 128) * pad(Ew, 128) * pad(K, 16)
+        prods = 4 if os.environ.get("KGE_XTILE_LOLO", "0") == "1" else 3
+        issued = 2.0 * prods * 2 * pad(ntest, 128) * pad(Ew, 128) * pad(K, 16)
         out[name] = {"ms": best * 1e3, "queries_per_s": 2 * ntest / best,
                      "bf16_issued_tflops": issued / best / 1e12, "peak_tflops": 2500.0,
                      "frac": issued / best / 1e12 / 2500.0,
                      "fp32_equivalent_tflops": flops / best / 1e12,
                      "what": "whole pass wall time (host filter CSR, bitmap, operand split, window, MFMA tile, "
                              "refinement, read-back); frac = issued bf16 MFMA flops / 2.5 PF bf16 dense spec",
-                     "path": "split-bf16 MFMA tile (4 bf16 products per fp32 product) + reference-order refinement",
+                     "path": f"split-bf16 MFMA tile ({prods} bf16 products per fp32 product) + reference-order "
+                             "refinement",
                      "mrr": float(np.mean(1.0 / np.concatenate([rh, rt])))}
         del m
     torch.cuda.empty_cache()

@@ -87,6 +87,7 @@ int rank_path(const kge_model_desc* m, int requested) {
   return x_ok ? RP_MFMA : mfma_ok ? RP_MFMA32 : (tile_ok ? RP_TILE : RP_SCAN);
 }
 constexpr int RANK_CAP = KGE_RANK_LIST_CAP;  // listed near-ties per query before the exact rescan takes over
+static_assert(RANK_CAP <= 1024, "k_rank_refine's pRotatE screen holds 4 list entries per thread of 256");
 
 Consts consts_of(const kge_model_desc* m) {
   Consts c;
@@ -1132,6 +1133,17 @@ int rank_impl(const kge_model_desc* m, int32_t mode, const int64_t* queries, int
     }
     if (st) return st;
     if (stage == RS_LIST) {  // the lists stay in the workspace for RS_ARGS / RS_FINISH
+      // pRotatE: the listed candidates re-scored with correctly rounded sin in
+      // the reference's order; those the library sin cannot move past the true
+      // score are counted now, only the rest go to the host (≈ 10× fewer)
+      RefArgs rs = ra;
+      rs.screen = env_int("KGE_RANK_SIN_SCREEN", 1) != 0 ? 1 : 0;
+      rs.ucnt_w = w.ucnt;
+      rs.ulist_w = w.ulist;
+      if (rs.screen) {
+        st = launch_status(ops.rank_ref(mode, 1, rs, s));
+        if (st) return st;
+      }
       ea.ranks = nullptr;
       ea.ties = nullptr;
       return launch_status(launch_rank_emit(ea, s));

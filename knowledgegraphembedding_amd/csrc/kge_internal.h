@@ -258,6 +258,10 @@ struct RefArgs {
   const float* sins;       // [item_off[nq], K] or null (refine / exact read it)
   float* args;             // [item_off[nq], K] (k_rank_sin_args writes it)
   int lib_sin;             // window: the reference sin is a library's (≤ 1 ulp), not correctly rounded
+  int screen;              // k_rank_refine (pRotatE, correctly rounded sin): count the listed candidates
+                           // that clear the library-sin bound, keep only the others in the list
+  int32_t* ucnt_w;         // (screen) the list, rewritten in place
+  int32_t* ulist_w;
 };
 
 // Register-tiled filtered ranking (kge_kernels.inc, k_rank_tile): 64 queries ×

@@ -19,7 +19,10 @@ What is asserted, per query (rank = 1 + #{unfiltered e ≠ true: s_e > s_true}):
     pRotatE's sin acts on per-candidate phase sums (model.py:241-245): the
     device lists the near-ties, writes their phase sums, the host takes the
     sin with the reference's own torch.sin (ops.reference_sin), and the device
-    re-scores them (kge_rank_sin_args / kge_rank_finish_sin).
+    re-scores them (kge_rank_sin_args / kge_rank_finish_sin); by default the
+    listed candidates are first re-scored with correctly rounded sin and only
+    those within the library sin's bound of the true score go to the host
+    ("auto/noscreen": all of them — the same ranks).
   * pRotatE with correctly rounded DEVICE sin (rank_trig = "device"): equal on
     every query decidable under the rigorous last-bit-of-sin bound δ below,
     within the competitors inside δ otherwise.
@@ -51,7 +54,7 @@ U = 2.0 ** -24
 EXACT = ("TransE", "DistMult", "ComplEx", "RotatE", "pRotatE")
 PATHS = {"DistMult": ("auto", "auto/lolo", "mfma32", "tile", "scan"),
          "ComplEx": ("auto", "auto/lolo", "mfma32", "tile", "scan"),
-         "TransE": ("auto", "scan"), "RotatE": ("auto", "scan"), "pRotatE": ("auto", "scan")}
+         "TransE": ("auto", "scan"), "RotatE": ("auto", "scan"), "pRotatE": ("auto", "auto/noscreen", "scan")}
 
 
 def build(name, E, R, d, gamma, seed):
@@ -125,10 +128,14 @@ def run_case(tag, name, E, R, d, gamma, seed, queries, filters, refs, report):
         base = None
         for path in PATHS[name]:
             import os
+            # "/lolo": the split tile with its lo·lo products; "/noscreen": pRotatE's
+            # listed candidates all go to the host sin (no correctly-rounded screen)
             os.environ["KGE_XTILE_LOLO"] = "1" if path.endswith("/lolo") else "0"
+            os.environ["KGE_RANK_SIN_SCREEN"] = "0" if path.endswith("/noscreen") else "1"
             ranks, ties, listed = m.rank_queries(qs, filters, mode, path=path.split("/")[0], listed=True,
                                                  relation_trig=trig)
             os.environ.pop("KGE_XTILE_LOLO", None)
+            os.environ.pop("KGE_RANK_SIN_SCREEN", None)
             if base is None:
                 base = (ranks, ties)
             else:
