@@ -437,6 +437,7 @@ int run_grad(const kge_model_desc* m, const Geom& geo, int mode, const int64_t* 
   ea.nsl = nsl;
   ea.slice_w = nsl > 0 ? (geo.eg.S + nsl - 1) / nsl : 0;
   ea.dma = (nsl > 0 && (double)B * Le * 4.0 < 2147483648.0 && env_int("KGE_ENT_DMA", 0) != 0) ? 1 : 0;
+  ea.variant = env_int("KGE_ENT_VARIANT", 0);
   ea.adam = adam_t(adam ? &adam->entity : nullptr);
   ea.adamk = ak;
   ea.align_sl = q_slm ? 0 : entity_slice_align(nsl, geo.eg.S, Le, m->entity_embedding, write_grad ? grad_entity : nullptr, ea.adam);
@@ -837,6 +838,7 @@ int kge_ship_step(const kge_model_desc* m, int32_t mode, const kge_ship_desc* sh
   ea.nsl = nsl;
   ea.slice_w = nsl > 0 ? (geo.eg.S + nsl - 1) / nsl : 0;
   ea.dma = (nsl > 0 && (double)B * Le * 4.0 < 2147483648.0 && env_int("KGE_ENT_DMA", 0) != 0) ? 1 : 0;
+  ea.variant = env_int("KGE_ENT_VARIANT", 0);
   ea.adam = adam_t(adam ? &adam->entity : nullptr);
   ea.adamk = ak;
   ea.B = B;

@@ -641,6 +641,245 @@ __global__ __launch_bounds__(128 * WM, WM == 4 ? 1 : (TQ == 1 ? 3 : 2)) void k_r
   if (t < X::BQ && arow[t] >= 0 && cgt[t]) atomicAdd(&a.gt[q0 + t], cgt[t]);
 }
 
+// Persistent counting pass (KGE_XTILE_PERSIST=1): two 256-thread workgroups
+// per CU for the whole launch, workgroup b running its XCD's tiles
+// i = b/8, b/8 + G/8, … in xcd_tile's group order.  The LDS ring runs on
+// across tiles: the first three slabs of tile t+1 are issued during tile t's
+// last three slabs, so they land during tile t's epilogue and no tile starts
+// on an empty ring.  Everything a tile's epilogue reads besides the scores —
+// s_true and the window per query, each lane's two exclusion-bitmap words —
+// arrives the same way, by LDS-DMA issued with the tile's first slab into one
+// of two metadata buffers, so the explicit vmcnt waits cover it (a plain
+// global load would make the compiler wait for every DMA issued after it).
+// Same slab arithmetic and epilogue as k_rank_mfma_x<false, 2>; needs
+// nslab ≥ 3 (a tile's metadata is issued once the previous tile's is read).
+struct XMeta {  // one metadata buffer (LDS)
+  float st[128], dl[128];
+  uint32_t ex[4][2][2][64];  // [wave][query tile j][candidate word i][lane]
+};
+
+__device__ __forceinline__ void xcd_tile_at(const XArgs& a, int k, int i, int& x, int& y) {
+  const int nxk = (a.gx - k + 7) >> 3;
+  const int per = a.group * a.gy;
+  const int g = i / per, rem = i - g * per;
+  const int gsz = min(a.group, nxk - g * a.group);
+  x = (g * a.group + rem % gsz) * 8 + k;
+  y = rem / gsz;
+}
+
+__device__ __forceinline__ __attribute__((address_space(3))) void* xp_lds(const void* p) {
+  return (__attribute__((address_space(3))) void*)p;
+}
+
+constexpr int XP_MAXT = 256;  // tiles per persistent workgroup (the launcher falls back above)
+
+template <bool LL>
+__global__ __launch_bounds__(256, 2) void k_rank_mfma_xp(XArgs a) {
+  constexpr int TQ = 2;
+  using X = XTile<TQ>;
+  __shared__ __attribute__((aligned(16))) uint16_t smem[XS_NST * X::STAGE];
+  __shared__ __attribute__((aligned(16))) XMeta meta[2];
+  __shared__ int32_t cgt[128];
+  __shared__ int32_t tcoord[XP_MAXT];  // this workgroup's tiles: tx << 16 | ty
+  const int t = threadIdx.x, lane = t & 63, w = wave_id();
+  const int wm = w >> 1, wn = w & 1;
+  const int kx = blockIdx.x & 7, i0 = blockIdx.x >> 3, istride = gridDim.x >> 3;
+  const int nxk = (a.gx - kx + 7) >> 3, ntile = nxk * a.gy;
+  const int my_tiles = (i0 < ntile) ? (ntile - i0 + istride - 1) / istride : 0;
+  if (my_tiles == 0) return;  // (block-uniform)
+  const int nslab = a.nslab;
+  const int total = my_tiles * nslab;
+  for (int k = t; k < my_tiles; k += 256) {
+    int tx, ty;
+    xcd_tile_at(a, kx, i0 + k * istride, tx, ty);
+    tcoord[k] = (tx << 16) | ty;
+  }
+  if (t < 128) cgt[t] = 0;
+  __syncthreads();
+  auto tile = [&](int it, int& tx, int& ty) {
+    const int v = __builtin_amdgcn_readfirstlane(tcoord[it]);
+    tx = v >> 16;
+    ty = v & 0xFFFF;
+  };
+  const auto rq = buf_rsrc(a.qs, a.qs_bytes);
+  const auto re = buf_rsrc(a.es, a.es_bytes);
+  const auto rst = buf_rsrc(a.s_true, (uint64_t)a.nq * 4u);
+  const auto rdl = buf_rsrc(a.win.delta, (uint64_t)a.nq * 4u);
+  const auto rbits = buf_rsrc(a.fbits, (uint64_t)a.nq * (uint64_t)a.W * 4u);
+  const int kh = lane >> 5, li = lane & 31;
+  const int wq0 = wn * 32 * TQ;
+  // the metadata of tile `it` into buffer it & 1 (issued before that tile's first slab)
+  auto issue_meta = [&](int it, int tx, int ty) {
+    XMeta& mb = meta[it & 1];
+    const int q0 = ty * X::BQ, e0 = tx * X::BNX;
+    if (w < 2) {
+      const int q = q0 + 64 * w + lane;
+      const uint32_t off = (q < a.nq) ? (uint32_t)q * 4u : XS_OOB;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rst, xp_lds(&mb.st[64 * w]), 4, off, 0, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rdl, xp_lds(&mb.dl[64 * w]), 4, off, 0, 0, 0);
+    }
+#pragma unroll
+    for (int j = 0; j < TQ; ++j)
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int q = q0 + wq0 + j * 32 + li;
+        const int widx = (e0 >> 5) + wm * 2 + i;
+        const uint32_t off = (q < a.nq && widx < a.W) ? (uint32_t)((uint64_t)q * (uint64_t)a.W + widx) * 4u : XS_OOB;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rbits, xp_lds(&mb.ex[w][j][i][0]), 4, off, 0, 0, 0);
+      }
+  };
+  // operand slabs in order g = 0, 1, …: (tile ni_it, slab ni_sl) into ring stage g % XS_NST
+  int ni_it = 0, ni_sl = 0, ng = 0;
+  auto issue_next = [&]() {
+    int tx, ty;
+    tile(ni_it, tx, ty);
+    if (ni_sl == 0) issue_meta(ni_it, tx, ty);
+    const int qrb = ty * X::BQ / 128;
+    const uint32_t qsub = (uint32_t)((ty * X::BQ) & 127) * 32;
+    uint16_t* base = smem + (ng % XS_NST) * X::STAGE;
+#pragma unroll
+    for (int k = 0; k < X::CPW; ++k) {
+      const int c = X::CPW * w + k;
+      uint32_t off;
+      const bool cand = c < 8;
+      if (cand) {
+        const int piece = (c >> 2) & 1, sub = c & 3;
+        off = (uint32_t)(((tx * nslab + ni_sl) * 2 + piece) * (2 * XS_PIECE) + sub * 1024 + lane * 16);
+      } else {
+        const int cc = c - 8, piece = cc / (2 * TQ), sub = cc % (2 * TQ);
+        off = (uint32_t)(((qrb * nslab + ni_sl) * 2 + piece) * (2 * XS_PIECE) + qsub + sub * 1024 + lane * 16);
+      }
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(cand ? re : rq, xp_lds(base + c * 512), 16, off, 0, 0, 0);
+    }
+    ++ng;
+    if (++ni_sl == nslab) {
+      ni_sl = 0;
+      ++ni_it;
+    }
+  };
+  // slab g has landed (and, with it, the metadata issued before it) once at
+  // most the operand DMAs of the (≤ 2) younger slabs are outstanding
+  auto wait_g = [&](int g) {
+    const int after = total - 1 - g;
+    if (after >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if (after == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  };
+  const f32x16 zero = {};
+#pragma unroll
+  for (int p = 0; p < XS_NST - 1; ++p)
+    if (p < total) issue_next();
+  int g = 0;
+  for (int it = 0; it < my_tiles; ++it) {
+    int tx, ty;
+    tile(it, tx, ty);
+    const int64_t q0 = (int64_t)ty * X::BQ, e0 = (int64_t)tx * X::BNX;
+    const bool live = q0 + wq0 < a.nq && e0 + wm * 64 < a.E;
+    f32x16 run[2][TQ], cor[2][TQ], mprev[2][TQ];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < TQ; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) run[i][j][r] = cor[i][j][r] = mprev[i][j][r] = 0.f;
+    for (int sl = 0; sl < nslab; ++sl, ++g) {
+      wait_g(g);
+      __builtin_amdgcn_s_barrier();  // every wave's DMA of slab g has landed; slab g-1's reads are done
+      if (ng < total) issue_next();  // slab g + XS_NST - 1
+      if (!live) continue;
+      const uint16_t* Eh = smem + (int)(g % XS_NST) * X::STAGE;
+      const uint16_t* El = Eh + XS_PIECE;
+      const uint16_t* Qh = Eh + 2 * XS_PIECE;
+      const uint16_t* Ql = Qh + TQ * 1024;
+      bf16x8 eh[2], el[2], qh[TQ], ql[TQ];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int row = wm * 64 + i * 32 + li;
+        eh[i] = *reinterpret_cast<const bf16x8*>(Eh + row * XS_BK + kh * 8);
+        el[i] = *reinterpret_cast<const bf16x8*>(El + row * XS_BK + kh * 8);
+      }
+#pragma unroll
+      for (int j = 0; j < TQ; ++j) {
+        const int row = wq0 + j * 32 + li;
+        qh[j] = *reinterpret_cast<const bf16x8*>(Qh + row * XS_BK + kh * 8);
+        ql[j] = *reinterpret_cast<const bf16x8*>(Ql + row * XS_BK + kh * 8);
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < TQ; ++j) {
+#pragma unroll
+          for (int r = 0; r < 16; r += 2) {
+            f32x2 x = {run[i][j][r], run[i][j][r + 1]};
+            const f32x2 y = {mprev[i][j][r], mprev[i][j][r + 1]};
+            x += y;
+            run[i][j][r] = x.x;
+            run[i][j][r + 1] = x.y;
+          }
+          mprev[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(eh[i], qh[j], zero, 0, 0, 0);
+          cor[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(eh[i], ql[j], cor[i][j], 0, 0, 0);
+          cor[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(el[i], qh[j], cor[i][j], 0, 0, 0);
+          if constexpr (LL) cor[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(el[i], ql[j], cor[i][j], 0, 0, 0);
+        }
+    }
+    // epilogue: the metadata of this tile landed with its first slab
+    const XMeta& mb = meta[it & 1];
+    if (live) {
+#pragma unroll
+      for (int j = 0; j < TQ; ++j) {
+        const int n = wq0 + j * 32 + li;
+        const int64_t q = q0 + n;
+        const float st = mb.st[n], dlt = mb.dl[n];
+        const int64_t widx0 = (e0 >> 5) + wm * 2;
+        uint32_t ex[2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          uint32_t word = (q < a.nq && widx0 + i < a.W) ? mb.ex[w][j][i][lane] : ~0u;
+          const int64_t valid = a.E - (e0 + wm * 64 + i * 32);
+          if (valid < 32) word |= (valid <= 0) ? ~0u : (~0u << valid);
+          ex[i] = word;
+        }
+        f32x16 acc[2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) acc[i] = (run[i][j] + mprev[i][j]) + cor[i][j];
+        int gcount = 0;
+        uint32_t near = 0;
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int mloc = (r & 3) + 8 * (r >> 2) + 4 * kh;
+            const bool ok = ((ex[i] >> mloc) & 1u) == 0u;
+            const float diff = acc[i][r] - st;
+            gcount += (ok && diff > dlt) ? 1 : 0;
+            near |= (ok && !(diff > dlt) && diff >= -dlt) ? (1u << (16 * i + r)) : 0u;
+          }
+        if (__builtin_amdgcn_ballot_w64(near != 0u)) {
+          while (near) {
+            const int b = __builtin_ctz(near);
+            near &= near - 1u;
+            const int i = b >> 4, r = b & 15;
+            const int mloc = (r & 3) + 8 * (r >> 2) + 4 * kh;
+            const int idx = atomicAdd(&a.win.ucnt[q], 1);
+            if (idx < a.win.cap) a.win.ulist[q * (int64_t)a.win.cap + idx] = (int32_t)(e0 + wm * 64 + i * 32 + mloc);
+          }
+        }
+        gcount += __shfl_xor(gcount, 32);
+        if (kh == 0 && q < a.nq && gcount) atomicAdd(&cgt[n], gcount);
+      }
+    }
+    // the tile's counts to global (one atomic per query); the LDS fence-free
+    // barrier keeps the next tile's DMAs in flight
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (t < X::BQ) {
+      const int c = cgt[t];
+      if (c && q0 + t < a.nq) atomicAdd(&a.gt[q0 + t], c);
+      cgt[t] = 0;
+    }
+  }
+}
+
 }  // namespace
 
 int launch_filter_bits(const int64_t* filt_off, const int64_t* filt_ids, const int64_t* true_id, int64_t nq,
@@ -725,6 +964,18 @@ int launch_rank_mfma_x(int gather, const uint16_t* qs, const uint16_t* es, int64
     } else {
       hipLaunchKernelGGL((k_rank_mfma_x<true, 1>), dim3(1, gy), dim3(256), 0, s, a);
     }
+    return (int)hipGetLastError();
+  }
+  // KGE_XTILE_PERSIST=1: the persistent form (TQ = 2, WM = 2, ≥ 3 slabs)
+  const char* pe = getenv("KGE_XTILE_PERSIST");
+  int dev = 0, ncu = 256;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) ncu = 256;
+  const unsigned gsz = (unsigned)(((2 * ncu) + 7) / 8 * 8);  // two workgroups per CU, a multiple of the 8 XCDs
+  const int64_t xp_tiles = ((a.gx + 7) / 8 * (int64_t)a.gy + gsz / 8 - 1) / (gsz / 8);  // per workgroup, XCD 0
+  if (tq == 2 && pe && atoi(pe) == 1 && a.nslab >= 3 && xp_tiles <= XP_MAXT && a.gx < 32768 && a.gy < 65536 &&
+      !(getenv("KGE_XTILE_WM") && atoi(getenv("KGE_XTILE_WM")) == 4)) {
+    if (xsplit_lolo()) hipLaunchKernelGGL((k_rank_mfma_xp<true>), dim3(gsz), dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((k_rank_mfma_xp<false>), dim3(gsz), dim3(256), 0, s, a);
     return (int)hipGetLastError();
   }
   // KGE_XTILE_WM=4: 256-candidate tiles, one 8-wave workgroup per CU (TQ = 2)

@@ -558,8 +558,9 @@ def test_entity_pass_column_slices_bitwise(name, d, B, monkeypatch):
             torch.testing.assert_close(l0[:4], l1[:4], rtol=1e-6, atol=0)
 
 
+@pytest.mark.parametrize("variant", ["0", "1", "2", "3", "4"])
 @pytest.mark.parametrize("name", NAMES)
-def test_occurrence_buckets_bitwise(name, monkeypatch):
+def test_occurrence_buckets_bitwise(name, variant, monkeypatch):
     """The single-call step's occurrence buckets (k_row's atomics, the entity
     pass sorting each bucket in registers, the relation rows found by
     scanning the batch) against the CSR (KGE_ENT_BUCKETS=0): the same
@@ -567,7 +568,9 @@ def test_occurrence_buckets_bitwise(name, monkeypatch):
     including entities whose occurrences overflow a bucket (> 64: entity 7 is
     every row's first three negatives, 192 times; entity 11 twice per row for
     32 rows) and are found by the scan of the whole batch instead, a
-    negative that is also a positive's head, and relations with many rows."""
+    negative that is also a positive's head, and relations with many rows.
+    Every variant of the bucket pass (KGE_ENT_VARIANT: moments loaded late,
+    6 or 8 q rows in flight) gives the same bits."""
     E, R, d, B, n = 300, 7, 200, 64, 40
     args = Namespace(negative_adversarial_sampling=True, adversarial_temperature=1.0, uni_weight=False,
                      regularization=1e-4 if name in ("ComplEx", "DistMult") else 0.0)
@@ -577,6 +580,7 @@ def test_occurrence_buckets_bitwise(name, monkeypatch):
     pos[:5, 0] = 7
     P, N, W = torch.from_numpy(pos).to(DEV), torch.from_numpy(neg).to(DEV), torch.from_numpy(w).to(DEV)
     out = {}
+    monkeypatch.setenv("KGE_ENT_VARIANT", variant)
     for bk in ("1", "0"):
         monkeypatch.setenv("KGE_ENT_BUCKETS", bk)
         m, *_ = build_model(name, E, R, d, 12.0, 5)
