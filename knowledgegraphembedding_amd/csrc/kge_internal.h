@@ -154,7 +154,7 @@ struct EntArgs {
   int align_sl;         // k_entity_sl: line-aligned 64-slot slices per row (entity_slice_align)
   const float* q_sl;    // k_entity_sl<.., QSL>: q slice-major (written by k_row; even slices only) or null
   int dma;              // k_entity_sl stages the q slices by LDS-DMA (needs B·Le·4 < 2^31)
-  int variant;          // k_entity_sl bucket path: 1 late moments, 2 eight q rows in flight, 3 both, 4 late + six (KGE_ENT_VARIANT)
+  int variant;          // k_entity_sl bucket path: 1 late moments, 2 eight q rows in flight, 3 both, 4 late + six, 5 wave-specialised (KGE_ENT_VARIANT)
   const int32_t* bkt;   // k_entity_sl<.., BK>: occurrence buckets [E, BKT_CAP] (instead of off / occ)
   const int32_t* bkt_cnt;  // [E]
   const int64_t* pos;   // BK, an overflowed bucket: the batch's ids, scanned in occurrence order

@@ -558,7 +558,7 @@ def test_entity_pass_column_slices_bitwise(name, d, B, monkeypatch):
             torch.testing.assert_close(l0[:4], l1[:4], rtol=1e-6, atol=0)
 
 
-@pytest.mark.parametrize("variant", ["0", "1", "2", "3", "4"])
+@pytest.mark.parametrize("variant", ["0", "1", "2", "3", "4", "5"])
 @pytest.mark.parametrize("name", NAMES)
 def test_occurrence_buckets_bitwise(name, variant, monkeypatch):
     """The single-call step's occurrence buckets (k_row's atomics, the entity
@@ -570,7 +570,8 @@ def test_occurrence_buckets_bitwise(name, variant, monkeypatch):
     32 rows) and are found by the scan of the whole batch instead, a
     negative that is also a positive's head, and relations with many rows.
     Every variant of the bucket pass (KGE_ENT_VARIANT: moments loaded late,
-    6 or 8 q rows in flight) gives the same bits."""
+    6 or 8 q rows in flight, wave-specialised gather and stream waves) gives
+    the same bits."""
     E, R, d, B, n = 300, 7, 200, 64, 40
     args = Namespace(negative_adversarial_sampling=True, adversarial_temperature=1.0, uni_weight=False,
                      regularization=1e-4 if name in ("ComplEx", "DistMult") else 0.0)
