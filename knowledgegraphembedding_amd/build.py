@@ -1,7 +1,11 @@
 """Build recipe for the HIP shared library (gfx950 only).
 
-    python -m knowledgegraphembedding_amd.build          # incremental
-    python -m knowledgegraphembedding_amd.build --clean  # full rebuild
+    python knowledgegraphembedding_amd/build.py          # incremental
+    python knowledgegraphembedding_amd/build.py --clean  # full rebuild
+
+(run as a file it does not import the package, whose __init__ loads the
+libraries being replaced; `python -m knowledgegraphembedding_amd.build` works
+while the existing libraries still load)
 
 Every csrc/*.hip translation unit is compiled with hipcc for
 --offload-arch=gfx950 in parallel and linked into

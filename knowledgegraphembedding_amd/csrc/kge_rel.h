@@ -55,8 +55,19 @@ __device__ __forceinline__ void rel_row_chunks(const RelArgs& a, int64_t rr, int
     }
     // the occurrences in order: the CSR bucket's, or (a.pos) the rows whose
     // relation is rr, found 64 batch rows at a time
+    // (a.pos: the relation ids of the next four 64-row chunks are loaded
+    // ahead in a register queue, so a wave's scan of a 1024-row batch waits
+    // on ≈4 load latencies, not 16)
     int64_t r0 = 0;
     uint64_t mask = 0;
+    auto rel_id = [&](int64_t ii) -> int64_t { return (ii < a.B) ? a.pos[ii * 3 + 1] : -1; };
+    int64_t v0 = -1, v1 = -1, v2 = -1, v3 = -1;
+    if (a.pos) {
+      v0 = rel_id(lane);
+      v1 = rel_id(64 + lane);
+      v2 = rel_id(128 + lane);
+      v3 = rel_id(192 + lane);
+    }
     while (true) {
       int64_t i;
       if (!a.pos) {
@@ -64,8 +75,11 @@ __device__ __forceinline__ void rel_row_chunks(const RelArgs& a, int64_t rr, int
         i = a.occ[p++] - a.Bn - 2 * a.B;
       } else {
         while (!mask && r0 < a.B) {
-          const int64_t ii = r0 + lane;
-          mask = __ballot(ii < a.B && a.pos[(ii < a.B ? ii : 0) * 3 + 1] == rr);
+          mask = __ballot(v0 == rr);
+          v0 = v1;
+          v1 = v2;
+          v2 = v3;
+          v3 = rel_id(r0 + 256 + lane);
           r0 += 64;
         }
         if (!mask) break;

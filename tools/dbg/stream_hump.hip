@@ -7,7 +7,9 @@
 // (as the entity pass), the default-policy stream, and the non-temporal
 // stream alternating with a 2.1 GB random-row read of a 120 MB table (k_row's
 // gather shape, table resident in the Infinity Cache).  One JSON line per
-// launch.
+// launch.  Variant 2 also times each gather launch (gather_us): a table kept
+// in the Infinity Cache between launches would show a cold first gather after
+// an idle gap if the cache were dropped while the GPU idles.
 //
 //   hipcc --offload-arch=gfx950 -O3 -o /tmp/stream_hump tools/dbg/stream_hump.hip
 #include <hip/hip_runtime.h>
@@ -91,14 +93,19 @@ int main() {
   CK(hipMemcpy(ids, hid.data(), hid.size() * 4, hipMemcpyHostToDevice));
   const long n4 = N / 4;
   const int grid = 4096, launches = 80;
-  std::vector<hipEvent_t> ev(2 * launches);
+  std::vector<hipEvent_t> ev(2 * launches), evg(2 * launches);
+  for (auto& e : evg) CK(hipEventCreate(&e));
   for (auto& e : ev) CK(hipEventCreate(&e));
   const char* names[3] = {"stream_nt", "stream_default", "stream_nt_after_gather"};
   for (int variant = 0; variant < 3; ++variant) {
     for (int idle_ms : {2000, 50}) {
       usleep(idle_ms * 1000);
       for (int r = 0; r < launches; ++r) {
-        if (variant == 2) hipLaunchKernelGGL(k_gather, dim3(B), dim3(256), 0, 0, (const f4*)p, ids, out, NNEG);
+        if (variant == 2) {
+          CK(hipEventRecord(evg[2 * r], 0));
+          hipLaunchKernelGGL(k_gather, dim3(B), dim3(256), 0, 0, (const f4*)p, ids, out, NNEG);
+          CK(hipEventRecord(evg[2 * r + 1], 0));
+        }
         CK(hipEventRecord(ev[2 * r], 0));
         if (variant == 1) hipLaunchKernelGGL((k_adam_stream<false>), dim3(grid), dim3(256), 0, 0, p, m, v, g, n4);
         else hipLaunchKernelGGL((k_adam_stream<true>), dim3(grid), dim3(256), 0, 0, p, m, v, g, n4);
@@ -108,8 +115,10 @@ int main() {
       for (int r = 0; r < launches; ++r) {
         float ms = 0.f;
         CK(hipEventElapsedTime(&ms, ev[2 * r], ev[2 * r + 1]));
-        printf("{\"variant\": \"%s\", \"idle_ms\": %d, \"launch\": %d, \"us\": %.1f}\n", names[variant], idle_ms, r,
-               ms * 1e3);
+        float gms = 0.f;
+        if (variant == 2) CK(hipEventElapsedTime(&gms, evg[2 * r], evg[2 * r + 1]));
+        printf("{\"variant\": \"%s\", \"idle_ms\": %d, \"launch\": %d, \"us\": %.1f, \"gather_us\": %.1f}\n",
+               names[variant], idle_ms, r, ms * 1e3, gms * 1e3);
       }
       fflush(stdout);
     }
