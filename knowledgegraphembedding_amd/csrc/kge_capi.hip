@@ -313,12 +313,14 @@ int run_grad(const kge_model_desc* m, const Geom& geo, int mode, const int64_t* 
   ra.q_sl = q_slm ? w.q_sl : nullptr;
   ra.q_sl_w = q_slm ? (geo.eg.S + nsl - 1) / nsl : 0;
   const bool rel_side = sd && !rel_fused;
-  // occurrence buckets filled by k_row instead of the CSR (KGE_ENT_BUCKETS,
-  // default on): the single-call step on the slice-major path, when the
+  // occurrence buckets filled by k_row instead of the CSR (KGE_ENT_BUCKETS=1;
+  // bit-identical): the single-call step on the slice-major path, when the
   // average bucket is far below its capacity (an overflowed bucket is still
   // exact, only slow).  No side stream: no fork marker, no join, nothing
-  // beside k_row.
-  const bool buckets = q_slm && env_int("KGE_ENT_BUCKETS", 1) != 0 &&
+  // beside k_row.  Off by default: it saves the ≈6.5 µs join but the entity
+  // pass pays ≈8-9 µs for the per-wave sort and the bucket reads, ≈1.3 %
+  // per step net (profiles/r04/train/).
+  const bool buckets = q_slm && env_int("KGE_ENT_BUCKETS", 0) != 0 &&
                        (double)B * (double)(n + 2) <= 32.0 * (double)m->nentity;
   ra.bkt = buckets ? w.bkt : nullptr;
   ra.bkt_cnt = buckets ? w.bkt_cnt : nullptr;

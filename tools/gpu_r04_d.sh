@@ -7,8 +7,9 @@ timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout
 timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r04d_smoke.log 2>&1 || exit $?
 timeout -k 10 400 python -u bench.py > gpurun_out/r04d_bench_default.json 2> gpurun_out/r04d_bench.err || exit $?
 bash tools/profile.sh > gpurun_out/r04d_profile.log 2>&1 || exit $?
-for V in 0 5; do
-  TAG=ent_v${V}_a COUNTERS="TD_TD_BUSY_sum TCP_PENDING_STALL_CYCLES_sum TCC_HIT_sum TCC_MISS_sum GRBM_GUI_ACTIVE" ENVS="KGE_ENT_VARIANT=$V" bash tools/pmc_kernel.sh > gpurun_out/r04d_pmc_v${V}_a.txt 2>&1 || exit $?
-  TAG=ent_v${V}_f COUNTERS="FETCH_SIZE" ENVS="KGE_ENT_VARIANT=$V" bash tools/pmc_kernel.sh > gpurun_out/r04d_pmc_v${V}_f.txt 2>&1 || exit $?
-  TAG=ent_v${V}_w COUNTERS="WRITE_SIZE" ENVS="KGE_ENT_VARIANT=$V" bash tools/pmc_kernel.sh > gpurun_out/r04d_pmc_v${V}_w.txt 2>&1 || exit $?
+for V in csr ws; do
+  if [ $V = csr ]; then E="KGE_ENT_BUCKETS=0"; else E="KGE_ENT_BUCKETS=1 KGE_ENT_VARIANT=5"; fi
+  TAG=ent_${V}_a COUNTERS="TD_TD_BUSY_sum TCP_PENDING_STALL_CYCLES_sum TCC_HIT_sum TCC_MISS_sum GRBM_GUI_ACTIVE" ENVS="$E" bash tools/pmc_kernel.sh > gpurun_out/r04d_pmc_${V}_a.txt 2>&1 || exit $?
+  TAG=ent_${V}_f COUNTERS="FETCH_SIZE" ENVS="$E" bash tools/pmc_kernel.sh > gpurun_out/r04d_pmc_${V}_f.txt 2>&1 || exit $?
+  TAG=ent_${V}_w COUNTERS="WRITE_SIZE" ENVS="$E" bash tools/pmc_kernel.sh > gpurun_out/r04d_pmc_${V}_w.txt 2>&1 || exit $?
 done
