@@ -16,6 +16,14 @@ Bursts "idle_ms:steps": after the first burst, the GPU idles idle_ms before
 the next one — whether the early-step phase returns after an idle gap in the
 same process, and after how long, separates a power-state effect from one of
 the process's own data.
+
+--clock-probe: the SMU's metrics table refreshes every ≈20 ms, too coarse for
+a phase of ≈10 steps (≈6 ms), so the shader clock is also read in-kernel:
+tools/dbg/libclock_probe.so's one-wave kernel runs on a second stream through
+each burst and samples (s_memrealtime, s_memtime) every few µs; each step's
+row-pass and entity-pass clock is Δtick / Δreal × 100 MHz over the samples
+inside that kernel's event-timed interval (placed on the probe's time axis by
+a marker kernel on the step stream just before the burst).
 """
 from __future__ import annotations
 
@@ -69,6 +77,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--bursts", default="0:150,1000:60,50:60,5000:60")
     ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--clock-probe", default=os.path.join(HERE, "dbg", "libclock_probe.so"),
+                    help="in-kernel clock probe library ('' = off)")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
@@ -99,6 +109,12 @@ def main():
         KGEModel.train_step(model, opt, it, args)
     torch.cuda.synchronize()
     lib = _lib.load()
+    probe = None
+    if a.clock_probe and os.path.exists(a.clock_probe):
+        probe = ctypes.CDLL(a.clock_probe)
+        probe.clock_probe_launch.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+        probe.marker_stamp.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+        probe_stream = torch.cuda.Stream(dev)
     samples, stop = [], threading.Event()
     th = threading.Thread(target=sampler, args=(handle, samples, stop), daemon=True)
     th.start()
@@ -110,6 +126,13 @@ def main():
         idle_ms, nsteps = (float(x) for x in spec.split(":"))
         nsteps = int(nsteps)
         time.sleep(idle_ms / 1e3)
+        if probe is not None:
+            nsamp = int((nsteps * 0.7 + 10.0) / 0.0035)  # ≈3.5 µs per sample (one s_sleep 127)
+            pbuf = torch.zeros(2 * nsamp, dtype=torch.int64, device=dev)
+            mbuf = torch.zeros(2, dtype=torch.int64, device=dev)
+            torch.cuda.synchronize()
+            assert probe.clock_probe_launch(pbuf.data_ptr(), nsamp, 1, ctypes.c_void_p(probe_stream.cuda_stream)) == 0
+            assert probe.marker_stamp(mbuf.data_ptr(), ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)) == 0
         _lib.check(lib.kge_stage_timer(1, None, 1), "kge_stage_timer")
         t_host0 = time.perf_counter()
         for _ in range(nsteps):
@@ -120,6 +143,21 @@ def main():
         _lib.check(lib.kge_stage_timer(3, buf.ctypes.data_as(ctypes.c_void_p), buf.size), "kge_stage_timer")
         lib.kge_stage_timer(0, None, 0)
         st = buf.reshape(nsteps, 7)
+        clk = None
+        if probe is not None:
+            torch.cuda.synchronize()
+            pv = pbuf.cpu().numpy().reshape(-1, 2).astype(np.float64)
+            mv = mbuf.cpu().numpy().astype(np.float64)
+            pv = pv[pv[:, 0] > 0]
+            t_ms = (pv[:, 0] - mv[0]) / 1e5  # 100 MHz constant counter → ms from the marker
+
+            def clock_mhz(t0, t1):
+                sel = np.nonzero((t_ms >= t0) & (t_ms <= t1))[0]
+                if len(sel) < 2:
+                    return None
+                i, j = sel[0], sel[-1]
+                return float((pv[j, 1] - pv[i, 1]) / (pv[j, 0] - pv[i, 0]) * 100.0)
+            clk = clock_mhz
         print(json.dumps({"burst": bi, "idle_ms_before": idle_ms, "steps": nsteps,
                           "host_span_ms": (t_host1 - t_host0) * 1e3,
                           "device_span_ms": float(st[-1, 6] + st[-1, :6].sum())}), flush=True)
@@ -134,8 +172,13 @@ def main():
                 if v:
                     agg[key] = float(np.mean(v))
             fts = sorted({s_["firmware_timestamp"] for s_ in win if "firmware_timestamp" in s_})
-            print(json.dumps({"burst": bi, "step": k, "row_ms": float(st[k, 1]), "entity_ms": float(st[k, 4]),
-                              "start_ms": float(st[k, 6]), "n_samples": len(win), "fw_stamps": len(fts), **agg}))
+            rec = {"burst": bi, "step": k, "row_ms": float(st[k, 1]), "entity_ms": float(st[k, 4]),
+                   "start_ms": float(st[k, 6]), "n_samples": len(win), "fw_stamps": len(fts), **agg}
+            if clk is not None:
+                s0 = float(st[k, 6])
+                rec["probe_row_mhz"] = clk(s0 + float(st[k, 0]), s0 + float(st[k, :2].sum()))
+                rec["probe_entity_mhz"] = clk(s0 + float(st[k, :4].sum()), s0 + float(st[k, :5].sum()))
+            print(json.dumps(rec))
     time.sleep(0.05)
     stop.set()
     th.join()
