@@ -284,6 +284,8 @@ def main():
     ap.add_argument("--no-rank", action="store_true", help="skip the config-3 ranking section (rank 0, 1 GPU)")
     ap.add_argument("--hidden-dim", type=int, default=None,
                     help="override the workload's hidden_dim (diagnostics; the headline is the workload's own)")
+    ap.add_argument("--batch", type=int, default=None,
+                    help="override the workload's batch size (diagnostics; the headline is the workload's own)")
     ap.add_argument("--traffic-json", default=None,
                     help="rocprofv3 PMC summary (tools/pmc_traffic.py output) for roofline.traffic "
                          "(default: the committed profiles/pmc_traffic.json of this workload)")
@@ -293,6 +295,8 @@ def main():
     E, R, D, B, NNEG = wl["E"], wl["R"], wl["D"], wl["B"], wl["NNEG"]
     if a.hidden_dim:
         D = a.hidden_dim
+    if a.batch:
+        B = a.batch
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -391,7 +395,7 @@ def main():
     row_traffic = ent_traffic = None
     # the committed PMC summaries and pattern ceilings were measured on the
     # workload's own shape (d = 1000): not applicable to a --hidden-dim run
-    own_shape = not a.hidden_dim or a.hidden_dim == wl["D"]
+    own_shape = (not a.hidden_dim or a.hidden_dim == wl["D"]) and (not a.batch or a.batch == wl["B"])
     if a.workload == "fb15k" and not exchanged and own_shape:  # PMC summaries of this workload (tools/profile.sh + tools/pmc_traffic.py)
         row_traffic = _pmc_bytes(a.traffic_json or os.path.join(here, "profiles", "pmc_traffic.json"))
         ent_traffic = _pmc_bytes(os.path.join(here, "profiles", "pmc_traffic_entity.json"))
