@@ -407,6 +407,21 @@ __device__ __forceinline__ bool xcd_tile(const XArgs& a, int& x, int& y) {
 // threads, 2 workgroups per CU) or 4 (256 candidates, 512 threads, one
 // workgroup per CU: the same 64×64 per wave, a third less L2 → LDS traffic
 // per MFMA — each slab's query piece feeds twice the candidates).
+// s_waitcnt vmcnt(n) for the DMA counts the ring loops need (n = slabs × CPW
+// with CPW 3 or 4 and ≤ 4 younger slabs); any other n waits for everything
+__device__ __forceinline__ void wait_vmcnt_dma(int n) {
+  switch (n) {
+    case 16: asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); break;
+    case 12: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
+    case 9: asm volatile("s_waitcnt vmcnt(9)" ::: "memory"); break;
+    case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+    case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+  }
+}
+
 template <int TQ, int WM = 2>
 struct XTile {
   static constexpr int BQ = 64 * TQ;                   // queries per workgroup
@@ -418,13 +433,17 @@ struct XTile {
   static_assert((4 * WM + 4 * TQ) % (2 * WM) == 0, "DMA chunks must split evenly over the waves");
 };
 
-template <bool GATHER, int TQ, int WM = 2, bool LL = true>
+// NST: LDS ring stages (NST − 1 slabs in flight).  4 by default; the
+// 256-candidate tile can hold 6 (144 KB of ring at one workgroup per CU:
+// KGE_XTILE_WM=4 KGE_XTILE_NST=6).
+template <bool GATHER, int TQ, int WM = 2, bool LL = true, int NST = XS_NST>
 __global__ __launch_bounds__(128 * WM, WM == 4 ? 1 : (TQ == 1 ? 3 : 2)) void k_rank_mfma_x(XArgs a) {
   using X = XTile<TQ, WM>;
   static_assert(!GATHER || WM == 2, "the gather pass uses 128-row candidate tiles");
-  // one LDS array: [XS_NST stages][E_hi | E_lo | Q_hi | Q_lo] then arow/brow, sts, sdl, cgt
-  __shared__ __attribute__((aligned(16))) uint16_t smem[XS_NST * X::STAGE + 128 * 4 * 2 + 128 * 2 * 2 + 128 * 2 * 3];
-  int64_t* arow = reinterpret_cast<int64_t*>(smem + XS_NST * X::STAGE);
+  static_assert(NST >= 3 && NST <= 6, "ring depth");
+  // one LDS array: [NST stages][E_hi | E_lo | Q_hi | Q_lo] then arow/brow, sts, sdl, cgt
+  __shared__ __attribute__((aligned(16))) uint16_t smem[NST * X::STAGE + 128 * 4 * 2 + 128 * 2 * 2 + 128 * 2 * 3];
+  int64_t* arow = reinterpret_cast<int64_t*>(smem + NST * X::STAGE);
   int64_t* brow = arow + 128;
   float* sts = reinterpret_cast<float*>(brow + 128);
   float* sdl = sts + 128;
@@ -492,19 +511,12 @@ __global__ __launch_bounds__(128 * WM, WM == 4 ? 1 : (TQ == 1 ? 3 : 2)) void k_r
     }
   };
   // DMAs issued after slab sl's, when sl is waited for: those of the next
-  // min(XS_NST − 2, nslab − 1 − sl) slabs, CPW instructions each (vmcnt counts in order)
+  // min(NST − 2, nslab − 1 − sl) slabs, CPW instructions each (vmcnt counts in order)
   static_assert(X::CPW == 3 || X::CPW == 4, "vmcnt immediates below");
   auto wait_slab = [&](int sl) {
-    const int after = nslab - 1 - sl;
-    if (after >= 2) {
-      if constexpr (X::CPW == 4) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-    } else if (after == 1) {
-      if constexpr (X::CPW == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
+    const int left = nslab - 1 - sl;
+    const int after = left < NST - 2 ? left : NST - 2;
+    wait_vmcnt_dma(after * X::CPW);
   };
 
   f32x16 run[2][TQ], cor[2][TQ], mprev[2][TQ];
@@ -535,15 +547,15 @@ __global__ __launch_bounds__(128 * WM, WM == 4 ? 1 : (TQ == 1 ? 3 : 2)) void k_r
       exw[j][i] = word;
     }
 #pragma unroll
-  for (int p = 0; p < XS_NST - 1; ++p)
+  for (int p = 0; p < NST - 1; ++p)
     if (p < nslab) issue(p, p);
   for (int sl = 0; sl < nslab; ++sl) {
     wait_slab(sl);                 // this wave's DMA of slab sl has landed
     __builtin_amdgcn_s_barrier();  // ... every wave's; slab sl-1's reads are done (no fence: the
                                    // vmcnt above covers the DMA, __syncthreads' would be vmcnt(0))
-    if (sl + XS_NST - 1 < nslab) issue(sl + XS_NST - 1, (sl + XS_NST - 1) % XS_NST);
+    if (sl + NST - 1 < nslab) issue(sl + NST - 1, (sl + NST - 1) % NST);
     if (!live) continue;
-    const uint16_t* Es = smem + (sl % XS_NST) * X::STAGE;
+    const uint16_t* Es = smem + (sl % NST) * X::STAGE;
     const uint16_t* Qh = Es + WM * XS_PIECE;
     const uint16_t* Ql = Qh + TQ * 1024;
     bf16x8 eh[2], el[2], qh[TQ], ql[TQ];
@@ -989,8 +1001,19 @@ int launch_rank_mfma_x(int gather, const uint16_t* qs, const uint16_t* es, int64
   const int64_t per_xcd = (int64_t)((a.gx + 7) / 8) * a.gy;  // XCD 0 has the most candidate tiles
   const dim3 gs((unsigned)(8 * per_xcd));
   if (wmv == 4) {
-    if (ll) hipLaunchKernelGGL((k_rank_mfma_x<false, 2, 4>), gs, dim3(512), 0, s, a);
-    else hipLaunchKernelGGL((k_rank_mfma_x<false, 2, 4, false>), gs, dim3(512), 0, s, a);
+    // KGE_XTILE_NST=6: a 6-stage ring (5 slabs in flight, 144 KB)
+    const char* nst_env = getenv("KGE_XTILE_NST");
+    const int nst = nst_env ? atoi(nst_env) : 4;
+    if (nst == 6) {
+      if (ll) hipLaunchKernelGGL((k_rank_mfma_x<false, 2, 4, true, 6>), gs, dim3(512), 0, s, a);
+      else hipLaunchKernelGGL((k_rank_mfma_x<false, 2, 4, false, 6>), gs, dim3(512), 0, s, a);
+    } else if (nst == 5) {
+      if (ll) hipLaunchKernelGGL((k_rank_mfma_x<false, 2, 4, true, 5>), gs, dim3(512), 0, s, a);
+      else hipLaunchKernelGGL((k_rank_mfma_x<false, 2, 4, false, 5>), gs, dim3(512), 0, s, a);
+    } else {
+      if (ll) hipLaunchKernelGGL((k_rank_mfma_x<false, 2, 4>), gs, dim3(512), 0, s, a);
+      else hipLaunchKernelGGL((k_rank_mfma_x<false, 2, 4, false>), gs, dim3(512), 0, s, a);
+    }
   } else if (!ll && tq == 2)
     hipLaunchKernelGGL((k_rank_mfma_x<false, 2, 2, false>), gs, dim3(256), 0, s, a);
   else if (tq == 1)
