@@ -216,6 +216,10 @@ __global__ __launch_bounds__(256, 4) void k_rank_mfma(MfmaArgs a) {
     // branch-free count; the rare near-ties collect in a bit mask and are
     // listed in one loop afterwards (a branch per candidate cost more than
     // the count itself)
+    // an excluded candidate's score becomes −∞ first: then "counted" is
+    // d > δ and "near" is |d| ≤ δ (−δ ≤ d ≤ δ; false for −∞ and NaN), the
+    // same sets as ok ∧ d > δ and ok ∧ ¬(d > δ) ∧ d ≥ −δ with fewer live
+    // compare masks
     int g = 0;
     uint32_t near = 0;  // bit 16·i + r
 #pragma unroll
@@ -223,10 +227,10 @@ __global__ __launch_bounds__(256, 4) void k_rank_mfma(MfmaArgs a) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int mloc = (r & 3) + 8 * (r >> 2) + 4 * kh;
-        const bool ok = ((ex[i] >> mloc) & 1u) == 0u;
-        const float diff = acc[i][j][r] - st;
-        g += (ok && diff > dlt) ? 1 : 0;
-        near |= (ok && !(diff > dlt) && diff >= -dlt) ? (1u << (16 * i + r)) : 0u;
+        const float sc = ((ex[i] >> mloc) & 1u) ? -__builtin_inff() : acc[i][j][r];
+        const float diff = sc - st;
+        g += (diff > dlt) ? 1 : 0;
+        near |= (__builtin_fabsf(diff) <= dlt) ? (1u << (16 * i + r)) : 0u;
       }
     if (__builtin_amdgcn_ballot_w64(near != 0u)) {
       while (near) {
@@ -642,6 +646,10 @@ __global__ __launch_bounds__(128 * WM, WM == 4 ? 1 : (TQ == 1 ? 3 : 2)) void k_r
     // branch-free count; the rare near-ties collect in a bit mask and are
     // listed in one loop afterwards (a branch per candidate cost more than
     // the count itself)
+    // an excluded candidate's score becomes −∞ first: then "counted" is
+    // d > δ and "near" is |d| ≤ δ (−δ ≤ d ≤ δ; false for −∞ and NaN), the
+    // same sets as ok ∧ d > δ and ok ∧ ¬(d > δ) ∧ d ≥ −δ with fewer live
+    // compare masks
     int g = 0;
     uint32_t near = 0;  // bit 16·i + r
 #pragma unroll
@@ -649,10 +657,10 @@ __global__ __launch_bounds__(128 * WM, WM == 4 ? 1 : (TQ == 1 ? 3 : 2)) void k_r
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int mloc = (r & 3) + 8 * (r >> 2) + 4 * kh;
-        const bool ok = ((ex[i] >> mloc) & 1u) == 0u;
-        const float diff = acc[i][j][r] - st;
-        g += (ok && diff > dlt) ? 1 : 0;
-        near |= (ok && !(diff > dlt) && diff >= -dlt) ? (1u << (16 * i + r)) : 0u;
+        const float sc = ((ex[i] >> mloc) & 1u) ? -__builtin_inff() : acc[i][j][r];
+        const float diff = sc - st;
+        g += (diff > dlt) ? 1 : 0;
+        near |= (__builtin_fabsf(diff) <= dlt) ? (1u << (16 * i + r)) : 0u;
       }
     if (__builtin_amdgcn_ballot_w64(near != 0u)) {
       while (near) {
