@@ -601,14 +601,7 @@ __global__ __launch_bounds__(128 * WM, WM == 4 ? 1 : (TQ == 1 ? 3 : 2)) void k_r
     for (int i = 0; i < 2; ++i)
 #pragma unroll
       for (int j = 0; j < TQ; ++j) {
-#pragma unroll
-        for (int r = 0; r < 16; r += 2) {
-          f32x2 x = {run[i][j][r], run[i][j][r + 1]};
-          const f32x2 y = {mprev[i][j][r], mprev[i][j][r + 1]};
-          x += y;
-          run[i][j][r] = x.x;
-          run[i][j][r + 1] = x.y;
-        }
+        run[i][j] += mprev[i][j];  // (v_pk_add_f32 pairs)
         mprev[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(eh[i], qh[j], zero, 0, 0, 0);
         cor[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(eh[i], ql[j], cor[i][j], 0, 0, 0);
         cor[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(el[i], qh[j], cor[i][j], 0, 0, 0);
