@@ -1068,6 +1068,7 @@ int rank_impl(const kge_model_desc* m, int32_t mode, const int64_t* queries, int
   ra.queries = queries; ra.nq = nq; ra.E = m->nentity; ra.R = m->nrelation;
   ra.Le = m->entity_dim; ra.Lr = m->relation_dim; ra.K = K; ra.c = a.c;
   ra.q = w.q; ra.qref = w.qref; ra.true_id = w.true_id; ra.s_true = w.s_true; ra.sref_true = w.sref_true;
+  ra.s_true_w = w.s_true;
   ra.delta = w.delta; ra.stats = w.stats;
   ra.exact_fast = (m->model == KGE_TRANSE && rp == RP_TILE) ? 1 : 0;
   ra.ucnt = w.ucnt; ra.ulist = w.ulist; ra.cap = RANK_CAP;
@@ -1105,11 +1106,14 @@ int rank_impl(const kge_model_desc* m, int32_t mode, const int64_t* queries, int
     ta.nq = nq; ta.E = m->nentity; ta.Le = m->entity_dim; ta.K = K;
     ta.c = a.c; ta.true_id = w.true_id; ta.s_true = w.s_true;
     ta.fbits = w.bits; ta.W = a.W; ta.gt = w.gt; ta.win = win;
+    // split-bf16 path: s_true in the reference's order after the window
+    // (k_rank_true_ref, KGE_RANK_TRUE_REF=0: the gather-mode tile here)
+    const bool true_ref = rp == RP_MFMA && ((m->entity_dim + 3) & ~3) <= 1024 && env_int("KGE_RANK_TRUE_REF", 1) != 0;
     if (rp == RP_MFMA) {
       st = launch_status(launch_split_bf16(w.q, nq, m->entity_dim, w.qs, s));
       if (!st)
         st = launch_status(launch_split_bf16(m->entity_embedding, m->nentity, m->entity_dim, w.es, s, w.tag + 6));
-      if (!st)
+      if (!st && !true_ref)
         st = launch_status(launch_rank_mfma_x(1, w.qs, w.es, nq, m->nentity, m->entity_dim, w.true_id, w.s_true,
                                               w.bits, w.gt, win, s));
     } else if (rp == RP_MFMA32)
@@ -1121,6 +1125,10 @@ int rank_impl(const kge_model_desc* m, int32_t mode, const int64_t* queries, int
     // 4. near-tie windows and the reference-order q
     st = launch_status(ops.rank_ref(mode, 0, ra, s));
     if (st) return st;
+    if (true_ref) {
+      st = launch_status(ops.rank_ref(mode, 4, ra, s));
+      if (st) return st;
+    }
     // 5. fast counting pass: clear cases counted, near-ties listed
     if (rp == RP_MFMA) {
       st = launch_status(launch_rank_mfma_x(0, w.qs, w.es, nq, m->nentity, m->entity_dim, w.true_id, w.s_true,
