@@ -1123,6 +1123,7 @@ int rank_impl(const kge_model_desc* m, int32_t mode, const int64_t* queries, int
       st = launch_status(ops.rank_tile(mode, 1, ta, s));
     if (st) return st;
     // 4. near-tie windows and the reference-order q
+    ra.true_exact = true_ref ? 1 : 0;
     st = launch_status(ops.rank_ref(mode, 0, ra, s));
     if (st) return st;
     if (true_ref) {

@@ -236,6 +236,7 @@ struct RefArgs {
   const float* s_true;     // [nq] fast-path true score
   float* sref_true;        // [nq] reference-order true score
   float* s_true_w;         // [nq] k_rank_true_ref writes s_true here (the split-bf16 path's true score)
+  int true_exact;          // s_true is the reference-order score (k_rank_true_ref): δ covers the candidate only
   float* delta;            // [nq] window
   const float* stats;      // [2] max row L2 norm, max |x| of the entity table
   int exact_fast;          // the fast pass is already in reference order (TransE on the register tile)
