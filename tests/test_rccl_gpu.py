@@ -1,5 +1,5 @@
 """Every data-parallel / row-partition exchange executed under RCCL (VERDICT
-r03 #4): a 1-rank "nccl" process group on cuda:0 inside the test process
+r03 #4): a 1-rank "nccl" process group on cuda:0 in one spawned child process
 (torch.distributed's nccl backend is RCCL on ROCm).  World 1 still takes each
 exchange's group code path — the async all-gathers / all-reduces /
 reduce-scatters, their work.wait() hand-offs onto the caller's stream, the
@@ -41,16 +41,56 @@ def _free_port():
     return p
 
 
-@pytest.fixture(scope="module")
-def rccl_group():
+# The group lives in ONE spawned child process for the whole module: an nccl
+# group in the pytest process leaves RCCL's threads behind after
+# destroy_process_group, and a later test that forks DataLoader workers
+# (test_run_gpu's run.py) can then hang in a child that inherited a held
+# lock.  The child runs every case, with and without the group, and hands the
+# results back through a file of its own (pickle of numpy arrays and floats).
+HOWS = ["factors", "owner", "grads", "rowpart-grads", "queries"]
+MODELS = [("RotatE", 0.0, False), ("pRotatE", 1e-4, True), ("ComplEx", 1e-4, False)]
+
+
+def _child(rank, out_path, port):
+    import pickle
     torch.cuda.set_device(0)
     os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{_free_port()}", rank=0, world_size=1,
-                            device_id=DEV)
-    try:
-        yield dist.group.WORLD
-    finally:
-        dist.destroy_process_group()
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1, device_id=DEV)
+    group = dist.group.WORLD
+    res = {}
+    t = torch.arange(5, dtype=torch.float32, device=DEV)
+    work = dist.all_reduce(t, async_op=True)
+    work.wait()
+    res["group"] = (dist.get_backend(group), dist.get_world_size(group), t.cpu().numpy(),
+                    str(torch.cuda.nccl.version()))
+    refs = {}
+    for name, reg, uni in MODELS:
+        refs[name] = _train(name, reg, uni)
+        for how in HOWS:
+            if how == "factors":
+                got = _train(name, reg, uni, group, dp_exchange="factors")
+            elif how == "owner":
+                got = _train(name, reg, uni, group, part_exchange="factors")
+            elif how == "grads":
+                got = _train(name, reg, uni, group, dp_exchange="grads")
+            elif how == "rowpart-grads":
+                got = _train(name, reg, uni, group, part_exchange="grads")
+            else:
+                got = _train(name, reg, uni, group, part_exchange="queries")
+            res[(how, name)] = (refs[name], got)
+    dist.destroy_process_group()
+    with open(out_path, "wb") as f:
+        pickle.dump(res, f)
+
+
+@pytest.fixture(scope="module")
+def rccl_results(tmp_path_factory):
+    import pickle
+    import torch.multiprocessing as mp
+    out = str(tmp_path_factory.mktemp("rccl") / "results.pkl")
+    mp.spawn(_child, args=(out, _free_port()), nprocs=1, join=True)
+    with open(out, "rb") as f:
+        return pickle.load(f)
 
 
 def _model(name):
@@ -90,31 +130,19 @@ def _train(name, reg, uni, group=None, dp_exchange=None, part_exchange=None):
             "mod": model.modulus.detach().cpu().numpy() if name == "pRotatE" else None}
 
 
-def test_group_is_rccl(rccl_group):
+def test_group_is_rccl(rccl_results):
     """The group really is RCCL, and a collective on a device tensor runs."""
-    assert dist.get_backend(rccl_group) == "nccl"
-    assert dist.get_world_size(rccl_group) == 1
-    t = torch.arange(5, dtype=torch.float32, device=DEV)
-    work = dist.all_reduce(t, async_op=True)
-    work.wait()
-    assert torch.equal(t.cpu(), torch.arange(5, dtype=torch.float32))
-    print("RCCL", torch.cuda.nccl.version())
+    backend, world, t, version = rccl_results["group"]
+    assert backend == "nccl"
+    assert world == 1
+    assert np.array_equal(t, np.arange(5, dtype=np.float32))
+    print("RCCL", version)
 
 
-@pytest.mark.parametrize("name,reg,uni", [("RotatE", 0.0, False), ("pRotatE", 1e-4, True), ("ComplEx", 1e-4, False)])
-@pytest.mark.parametrize("how", ["factors", "owner", "grads", "rowpart-grads", "queries"])
-def test_exchange_under_rccl(rccl_group, how, name, reg, uni):
-    ref = _train(name, reg, uni)
-    if how == "factors":
-        got = _train(name, reg, uni, rccl_group, dp_exchange="factors")
-    elif how == "owner":
-        got = _train(name, reg, uni, rccl_group, part_exchange="factors")
-    elif how == "grads":
-        got = _train(name, reg, uni, rccl_group, dp_exchange="grads")
-    elif how == "rowpart-grads":
-        got = _train(name, reg, uni, rccl_group, part_exchange="grads")
-    else:
-        got = _train(name, reg, uni, rccl_group, part_exchange="queries")
+@pytest.mark.parametrize("name,reg,uni", MODELS)
+@pytest.mark.parametrize("how", HOWS)
+def test_exchange_under_rccl(rccl_results, how, name, reg, uni):
+    ref, got = rccl_results[(how, name)]
     bitwise = how in ("factors", "owner")
     for k in ("ent", "rel") + (("mod",) if name == "pRotatE" else ()):
         if bitwise:
