@@ -165,49 +165,9 @@ static inline unsigned grid_for(int64_t n, unsigned cap = 4096) {
   return (unsigned)(g < cap ? g : cap);
 }
 
-// Bucket offsets up to 256 k buckets: one 1024-thread workgroup scans them
-// (each thread a contiguous run: its sum, the block scan of the sums, then
-// the run's prefixes).  The CSR runs beside k_row on a side stream, where
-// rocPRIM's multi-block look-back scan starved for free slots took 186-220
-// µs for FB15k's 16 k counts (profiles/r03/final/timeline_3steps.txt); one
-// workgroup needs one slot.  Integer and exact: the same offsets.
-constexpr int64_t SCAN_1BLK_MAX = 1 << 18;
-__global__ __launch_bounds__(1024) void k_scan_1blk(const int32_t* __restrict__ in, int32_t* __restrict__ out,
-                                                    int64_t n) {
-  __shared__ int32_t wsum[16];
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  const int64_t per = (n + 1023) / 1024;
-  const int64_t b = (int64_t)t * per, e = (b + per < n) ? b + per : n;
-  int32_t own = 0;
-  for (int64_t i = b; i < e; ++i) own += in[i];
-  int32_t x = own;  // inclusive scan over the wave
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const int32_t y = __shfl_up(x, o);
-    if (lane >= o) x += y;
-  }
-  if (lane == 63) wsum[w] = x;
-  __syncthreads();
-  if (t == 0) {
-    int32_t run = 0;
-    for (int k = 0; k < 16; ++k) {
-      const int32_t v = wsum[k];
-      wsum[k] = run;
-      run += v;
-    }
-  }
-  __syncthreads();
-  int32_t base = wsum[w] + x - own;  // exclusive prefix of this thread's run
-  for (int64_t i = b; i < e; ++i) {
-    const int32_t v = in[i];
-    out[i] = base;
-    base += v;
-  }
-}
-
 // Bucket offsets: a device-wide exclusive scan of cnt[0..nb] (cnt[nb] = 0, so
-// off[nb] = total) — k_scan_1blk up to SCAN_1BLK_MAX entries, rocPRIM's
-// decoupled look-back scan above (its scratch from the caller's workspace).
+// off[nb] = total) — rocPRIM's decoupled look-back scan, integer and exact;
+// its scratch comes from the caller's workspace.
 size_t csr_scan_temp_bytes(int64_t nb) {
   static thread_local int64_t last_nb = -1;  // the query is per size; remember the last one
   static thread_local size_t last_bytes = 0;
@@ -227,14 +187,9 @@ int launch_csr(const CsrArgs& a, hipStream_t s) {
   hipError_t e = hipMemsetAsync(a.cnt, 0, sizeof(int32_t) * (nb + 1), s);
   if (e != hipSuccess) return (int)e;
   hipLaunchKernelGGL(k_csr_hist, dim3(grid_for(N)), dim3(256), 0, s, a);
-  if (nb + 1 <= SCAN_1BLK_MAX && getenv("KGE_CSR_ROCPRIM") == nullptr) {
-    hipLaunchKernelGGL(k_scan_1blk, dim3(1), dim3(1024), 0, s, a.cnt, a.off, nb + 1);
-  } else {
-    size_t bytes = a.scan_tmp_bytes;
-    e = rocprim::exclusive_scan(a.scan_tmp, bytes, a.cnt, a.off, int32_t(0), (size_t)nb + 1, rocprim::plus<int32_t>(),
-                                s);
-    if (e != hipSuccess) return (int)e;
-  }
+  size_t bytes = a.scan_tmp_bytes;
+  e = rocprim::exclusive_scan(a.scan_tmp, bytes, a.cnt, a.off, int32_t(0), (size_t)nb + 1, rocprim::plus<int32_t>(), s);
+  if (e != hipSuccess) return (int)e;
   hipLaunchKernelGGL(k_csr_fill, dim3(grid_for(N)), dim3(256), 0, s, a);
   hipLaunchKernelGGL(k_csr_rank_w, dim3((unsigned)((nb + 3) / 4)), dim3(256), 0, s, a, nb);
   return (int)hipGetLastError();
