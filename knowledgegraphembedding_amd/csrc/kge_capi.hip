@@ -1078,7 +1078,14 @@ int rank_impl(const kge_model_desc* m, int32_t mode, const int64_t* queries, int
   ra.lib_sin = (stage != RS_ALL) ? 1 : 0;
   // the split-bf16 tile's error bound in units of u·‖q‖·max‖e‖ (kge_rank_mfma.hip)
   const int64_t xns = xsplit_nslab(m->entity_dim);
-  ra.fast_u = (rp == RP_MFMA) ? (float)(546.0 + 1.02 * xns + 0.05 * xns * 16 + (xsplit_lolo() ? 0.0 : 64.2)) : 0.f;
+  // the split tile's bound in u·‖q‖·max‖e‖ (kge_rank_mfma.hip): splitting 512.1, hi·hi MFMAs 32.3, running
+  // sum 1.02·nslab, correction chain 0.0472·Kp, final add 1.01 (+64.2 with the lo·lo products dropped);
+  // KGE_XTILE_MERGE: the corrections inside each slab's hi·hi chain, 3 (4) chained MFMAs of ≤ 32u
+  // each on partial sums ≤ (1 + 2^-8)·P_slab: 96.5 (128.5) in place of 32.3 + 0.0472·Kp
+  const bool lolo = xsplit_lolo();
+  ra.fast_u = (rp != RP_MFMA) ? 0.f
+              : xsplit_merge() ? (float)(513.2 + (lolo ? 128.5 : 96.5) + 1.02 * xns + (lolo ? 0.0 : 64.2))
+                               : (float)(546.0 + 1.02 * xns + 0.05 * xns * 16 + (lolo ? 0.0 : 64.2));
   if (stage == RS_ARGS) return launch_status(ops.rank_ref(mode, 3, ra, s));
   EmitArgs ea;
   ea.gt = w.gt; ea.eq = w.eq; ea.gtx = w.gtx; ea.eqx = w.eqx; ea.ucnt = w.ucnt; ea.true_id = w.true_id;

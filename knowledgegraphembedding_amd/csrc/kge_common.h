@@ -30,6 +30,7 @@ int64_t xsplit_nslab(int K);
 // the split tile's lo·lo products (KGE_XTILE_LOLO, default 0: dropped — three
 // MFMAs per product instead of four, +64.2·u·P on the error bound; 1 keeps them)
 bool xsplit_lolo();
+bool xsplit_merge();
 int64_t xsplit_elems(int64_t rows, int K);
 int launch_split_bf16(const float* src, int64_t rows, int K, uint16_t* dst, hipStream_t s,
                       const int64_t* skip = nullptr);

@@ -445,8 +445,12 @@ struct XTile {
 // NST: LDS ring stages (NST − 1 slabs in flight).  4 by default; the
 // 256-candidate tile can hold 6 (144 KB of ring at one workgroup per CU:
 // KGE_XTILE_WM=4 KGE_XTILE_NST=6).
-template <bool GATHER, int TQ, int WM = 2, bool LL = true, int NST = XS_NST>
-__global__ __launch_bounds__(128 * WM, WM == 4 ? 1 : (TQ == 1 ? 3 : 2)) void k_rank_mfma_x(XArgs a) {
+// MRG (default; KGE_XTILE_MERGE=0 off): the correction products join each slab's hi·hi
+// chain (one accumulator per 32×32 block instead of two: ≈170 VGPRs, three
+// workgroups per CU on a 3-stage ring); the window's bound grows by the
+// chain's rounding (launch_rank_mfma_x's caller, fast_u).
+template <bool GATHER, int TQ, int WM = 2, bool LL = true, int NST = XS_NST, bool MRG = false>
+__global__ __launch_bounds__(128 * WM, WM == 4 ? 1 : (MRG ? 3 : (TQ == 1 ? 3 : 2))) void k_rank_mfma_x(XArgs a) {
   using X = XTile<TQ, WM>;
   static_assert(!GATHER || WM == 2, "the gather pass uses 128-row candidate tiles");
   static_assert(NST >= 3 && NST <= 6, "ring depth");
@@ -603,16 +607,25 @@ __global__ __launch_bounds__(128 * WM, WM == 4 ? 1 : (TQ == 1 ? 3 : 2)) void k_r
       for (int j = 0; j < TQ; ++j) {
         run[i][j] += mprev[i][j];  // (v_pk_add_f32 pairs)
         mprev[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(eh[i], qh[j], zero, 0, 0, 0);
-        cor[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(eh[i], ql[j], cor[i][j], 0, 0, 0);
-        cor[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(el[i], qh[j], cor[i][j], 0, 0, 0);
-        if constexpr (LL) cor[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(el[i], ql[j], cor[i][j], 0, 0, 0);
+        if constexpr (MRG) {
+          mprev[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(eh[i], ql[j], mprev[i][j], 0, 0, 0);
+          mprev[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(el[i], qh[j], mprev[i][j], 0, 0, 0);
+          if constexpr (LL) mprev[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(el[i], ql[j], mprev[i][j], 0, 0, 0);
+        } else {
+          cor[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(eh[i], ql[j], cor[i][j], 0, 0, 0);
+          cor[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(el[i], qh[j], cor[i][j], 0, 0, 0);
+          if constexpr (LL) cor[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(el[i], ql[j], cor[i][j], 0, 0, 0);
+        }
       }
   }
   f32x16 acc[2][TQ];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int j = 0; j < TQ; ++j) acc[i][j] = (run[i][j] + mprev[i][j]) + cor[i][j];
+    for (int j = 0; j < TQ; ++j) {
+      if constexpr (MRG) acc[i][j] = run[i][j] + mprev[i][j];
+      else acc[i][j] = (run[i][j] + mprev[i][j]) + cor[i][j];
+    }
 
   // C/D layout as the fp32 tile: col (query) = lane & 31, row (candidate) = (reg & 3) + 8·(reg >> 2) + 4·(lane >> 5)
   if (GATHER) {
@@ -959,6 +972,16 @@ bool xsplit_lolo() {  // default: dropped (9 % faster tile, profiles/r04/rank/ab
   const char* e = getenv("KGE_XTILE_LOLO");
   return e && atoi(e) == 1;
 }
+// default: corrections in the hi·hi chain on the 128-candidate tile (9 %
+// faster, three workgroups per CU; profiles/r04/rank/ab_merged_corrections.txt);
+// KGE_XTILE_MERGE=0: the separate correction accumulator
+bool xsplit_merge() {
+  const char* e = getenv("KGE_XTILE_MERGE");
+  const char* wm = getenv("KGE_XTILE_WM");
+  const char* tq = getenv("KGE_XTILE_TQ");
+  const char* pe = getenv("KGE_XTILE_PERSIST");
+  return !(e && atoi(e) == 0) && !(wm && atoi(wm) == 4) && !(tq && atoi(tq) == 1) && !(pe && atoi(pe) == 1);
+}
 int64_t xsplit_elems(int64_t rows, int K) { return ((rows + 127) / 128) * 128 * xsplit_nslab(K) * XS_BK * 2; }
 
 int launch_split_bf16(const float* src, int64_t rows, int K, uint16_t* dst, hipStream_t s, const int64_t* skip) {
@@ -1034,6 +1057,9 @@ int launch_rank_mfma_x(int gather, const uint16_t* qs, const uint16_t* es, int64
       if (ll) hipLaunchKernelGGL((k_rank_mfma_x<false, 2, 4>), gs, dim3(512), 0, s, a);
       else hipLaunchKernelGGL((k_rank_mfma_x<false, 2, 4, false>), gs, dim3(512), 0, s, a);
     }
+  } else if (tq == 2 && xsplit_merge()) {
+    if (ll) hipLaunchKernelGGL((k_rank_mfma_x<false, 2, 2, true, 3, true>), gs, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((k_rank_mfma_x<false, 2, 2, false, 3, true>), gs, dim3(256), 0, s, a);
   } else if (!ll && tq == 2)
     hipLaunchKernelGGL((k_rank_mfma_x<false, 2, 2, false>), gs, dim3(256), 0, s, a);
   else if (tq == 1)

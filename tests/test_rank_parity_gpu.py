@@ -52,8 +52,8 @@ pytestmark = pytest.mark.gpu
 DEV = torch.device("cuda", 0)
 U = 2.0 ** -24
 EXACT = ("TransE", "DistMult", "ComplEx", "RotatE", "pRotatE")
-PATHS = {"DistMult": ("auto", "auto/lolo", "auto/persist", "auto/wm4n6", "auto/gatherst", "mfma32", "tile", "scan"),
-         "ComplEx": ("auto", "auto/lolo", "auto/persist", "auto/wm4n6", "auto/gatherst", "mfma32", "tile", "scan"),
+PATHS = {"DistMult": ("auto", "auto/lolo", "auto/persist", "auto/wm4n6", "auto/gatherst", "auto/merge", "mfma32", "tile", "scan"),
+         "ComplEx": ("auto", "auto/lolo", "auto/persist", "auto/wm4n6", "auto/gatherst", "auto/merge", "mfma32", "tile", "scan"),
          "TransE": ("auto", "scan"), "RotatE": ("auto", "scan"), "pRotatE": ("auto", "auto/noscreen", "scan")}
 
 
@@ -135,6 +135,7 @@ def run_case(tag, name, E, R, d, gamma, seed, queries, filters, refs, report):
             os.environ["KGE_XTILE_WM"] = "4" if path.endswith("/wm4n6") else "2"
             os.environ["KGE_XTILE_NST"] = "6" if path.endswith("/wm4n6") else "4"
             os.environ["KGE_RANK_TRUE_REF"] = "0" if path.endswith("/gatherst") else "1"
+            os.environ["KGE_XTILE_MERGE"] = "1" if path.endswith("/merge") else "0"
             os.environ["KGE_RANK_SIN_SCREEN"] = "0" if path.endswith("/noscreen") else "1"
             ranks, ties, listed = m.rank_queries(qs, filters, mode, path=path.split("/")[0], listed=True,
                                                  relation_trig=trig)
@@ -143,6 +144,7 @@ def run_case(tag, name, E, R, d, gamma, seed, queries, filters, refs, report):
             os.environ.pop("KGE_XTILE_WM", None)
             os.environ.pop("KGE_XTILE_NST", None)
             os.environ.pop("KGE_RANK_TRUE_REF", None)
+            os.environ.pop("KGE_XTILE_MERGE", None)
             os.environ.pop("KGE_RANK_SIN_SCREEN", None)
             if base is None:
                 base = (ranks, ties)
@@ -283,7 +285,7 @@ def test_host_sin_matches_reference(golden_info, g_full, capsys):
     assert differ == 0.0, "this host's sin differs from the reference's: pRotatE ranks would follow this host's"
 
 
-@pytest.mark.parametrize("wm", ["2", "2/lolo", "4", "2/persist", "4/nst6", "2/gatherst"])
+@pytest.mark.parametrize("wm", ["2", "2/lolo", "4", "2/persist", "4/nst6", "2/gatherst", "2/merge", "2/merge-lolo"])
 @pytest.mark.parametrize("name,E,d", [("DistMult", 300, 50), ("DistMult", 257, 37), ("DistMult", 1000, 130),
                                       ("ComplEx", 300, 25), ("ComplEx", 513, 33), ("DistMult", 129, 16)])
 def test_split_bf16_tile_matches_other_paths(name, E, d, wm, monkeypatch):
@@ -303,12 +305,17 @@ def test_split_bf16_tile_matches_other_paths(name, E, d, wm, monkeypatch):
     falls back to the plain kernel); "nst6": the 256-candidate tile with a
     6-stage LDS ring (KGE_XTILE_WM=4 KGE_XTILE_NST=6); "gatherst": s_true from
     the gather-mode tile (KGE_RANK_TRUE_REF=0) instead of the reference-order
-    true score."""
+    true score; "merge": the corrections inside each slab's hi·hi chain, three
+    workgroups per CU (KGE_XTILE_MERGE=1), with and without the lo·lo
+    products."""
     monkeypatch.setenv("KGE_XTILE_WM", wm.split("/")[0])
     monkeypatch.setenv("KGE_XTILE_LOLO", "1" if wm.endswith("lolo") else "0")
     monkeypatch.setenv("KGE_XTILE_PERSIST", "1" if wm.endswith("persist") else "0")
     monkeypatch.setenv("KGE_XTILE_NST", "6" if wm.endswith("nst6") else "4")
     monkeypatch.setenv("KGE_RANK_TRUE_REF", "0" if wm.endswith("gatherst") else "1")
+    monkeypatch.setenv("KGE_XTILE_MERGE", "1" if "merge" in wm else "0")
+    if wm.endswith("merge-lolo"):
+        monkeypatch.setenv("KGE_XTILE_LOLO", "1")
     R = 7
     m, ent, rel, _, _ = build(name, E, R, d, 12.0, 17)
     with torch.no_grad():
@@ -331,7 +338,7 @@ def test_split_bf16_tile_matches_other_paths(name, E, d, wm, monkeypatch):
             assert np.array_equal(r, r0) and np.array_equal(t, t0), (name, E, d, mode, p)
 
 
-@pytest.mark.parametrize("wm", ["2", "2/lolo", "4", "2/persist", "4/nst6", "2/gatherst"])
+@pytest.mark.parametrize("wm", ["2", "2/lolo", "4", "2/persist", "4/nst6", "2/gatherst", "2/merge", "2/merge-lolo"])
 @pytest.mark.parametrize("name", ["DistMult", "ComplEx"])
 def test_split_bf16_tile_wide_dynamic_range(name, wm, monkeypatch):
     """The split tile's error bound is rigorous, not statistical: entity and
@@ -343,6 +350,9 @@ def test_split_bf16_tile_wide_dynamic_range(name, wm, monkeypatch):
     monkeypatch.setenv("KGE_XTILE_PERSIST", "1" if wm.endswith("persist") else "0")
     monkeypatch.setenv("KGE_XTILE_NST", "6" if wm.endswith("nst6") else "4")
     monkeypatch.setenv("KGE_RANK_TRUE_REF", "0" if wm.endswith("gatherst") else "1")
+    monkeypatch.setenv("KGE_XTILE_MERGE", "1" if "merge" in wm else "0")
+    if wm.endswith("merge-lolo"):
+        monkeypatch.setenv("KGE_XTILE_LOLO", "1")
     E, R, d = 500, 5, 48
     m, ent, rel, _, _ = build(name, E, R, d, 12.0, 23)
     g = np.random.default_rng(11)
