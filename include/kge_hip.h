@@ -438,6 +438,13 @@ int kge_rank_filtered(const kge_model_desc *m, int32_t mode, const int64_t *quer
  * count and the lists stay in the workspace for kge_rank_sin_args /
  * kge_rank_finish_sin below. */
 #define KGE_RANK_STAGE_LIST 0x200
+/* path | KGE_RANK_FILTER_TABLE: filt_off / filt_ids are the whole filter
+ * index instead of per-query lists: filt_off [E·R + 1] int64 start offsets,
+ * by key h·R + r (tail-batch) or r·E + t (head-batch), into filt_ids — every
+ * true triple's tail (tail-batch) or head (head-batch), sorted by key.  The
+ * device looks each query's list up itself (no per-query CSR on the host);
+ * the same ranks and ties. */
+#define KGE_RANK_FILTER_TABLE 0x400
 #define KGE_RANK_LIST_CAP 1024 /* listed near-ties per query; above it the query is rescanned in full */
 int kge_rank_filtered_ex(const kge_model_desc *m, int32_t mode, const int64_t *queries, int64_t nq,
                          const int64_t *filt_off, const int64_t *filt_ids, int64_t *ranks_out,

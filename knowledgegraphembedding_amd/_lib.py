@@ -20,6 +20,7 @@ DEVERR_SAMPLER = 2
 DEVERR_ARG = 4
 ABI_VERSION = "0.2"  # KGE_ABI_VERSION of the include/kge_hip.h this binding mirrors
 RANK_STAGE_LIST = 0x200  # KGE_RANK_STAGE_LIST
+RANK_FILTER_TABLE = 0x400  # KGE_RANK_FILTER_TABLE
 RANK_LIST_CAP = 1024  # KGE_RANK_LIST_CAP
 PHASE_ROWS, PHASE_ENTITY, PHASE_FINALIZE, PHASE_ALL = 1, 2, 4, 7
 SHIP_Q, SHIP_ROWS, SHIP_MERGE, SHIP_CHAIN, SHIP_ENTITY = 1, 2, 3, 4, 5

@@ -1028,7 +1028,8 @@ int rank_impl(const kge_model_desc* m, int32_t mode, const int64_t* queries, int
   // KGE_RANK_REUSE_TABLE: the workspace already holds this entity table's
   // statistics and split operands from the previous call (the other direction)
   const bool reuse = (path & KGE_RANK_REUSE_TABLE) != 0;
-  path &= ~(KGE_RANK_REUSE_TABLE | KGE_RANK_STAGE_LIST);
+  const bool ftab = (path & KGE_RANK_FILTER_TABLE) != 0;  // filt_off / filt_ids: the whole filter index
+  path &= ~(KGE_RANK_REUSE_TABLE | KGE_RANK_STAGE_LIST | KGE_RANK_FILTER_TABLE);
   if (path < RP_AUTO || path > RP_MFMA32) return KGE_ERR_ARG;
   if (nq == 0) return KGE_OK;
   if (nq > 65535) return KGE_ERR_DIM;  // the bitmap launch puts queries on grid.y
@@ -1095,7 +1096,11 @@ int rank_impl(const kge_model_desc* m, int32_t mode, const int64_t* queries, int
     st = launch_status(ops.rank(mode, geo.vec, geo.ns, a, s));
     if (st) return st;
     // 2. excluded candidates (filtered ids + the true id) as a bitmap
-    st = launch_status(launch_filter_bits(filt_off, filt_ids, w.true_id, nq, m->nentity, w.bits, err_flag, s));
+    if (ftab)
+      st = launch_status(launch_filter_bits_tab(queries, mode == KGE_HEAD_BATCH ? 1 : 0, filt_off, filt_ids, w.true_id,
+                                                nq, m->nentity, m->nrelation, w.bits, err_flag, s));
+    else
+      st = launch_status(launch_filter_bits(filt_off, filt_ids, w.true_id, nq, m->nentity, w.bits, err_flag, s));
     if (st) return st;
     // the table's statistics and split operands: reused only where the tag
     // says this workspace already holds them for this table (k_rank_tag)

@@ -43,6 +43,9 @@ int launch_table_stats(const float* ent, int64_t E, int Le, float* stats, hipStr
 // the ranking workspace's table tag (KGE_RANK_REUSE_TABLE; kge_rank_mfma.hip k_rank_tag)
 int launch_rank_tag(int64_t* tag, const float* ent, int64_t E, int Le, int reuse, int need_stats, int need_split,
                     hipStream_t s);
+int launch_filter_bits_tab(const int64_t* queries, int head, const int64_t* tab, const int64_t* vals,
+                           const int64_t* true_id, int64_t nq, int64_t E, int64_t R, uint32_t* bits, int32_t* err,
+                           hipStream_t s);
 int launch_filter_bits(const int64_t* filt_off, const int64_t* filt_ids, const int64_t* true_id, int64_t nq,
                        int64_t E, uint32_t* bits, int32_t* err, hipStream_t s);
 struct EmitArgs {

@@ -270,6 +270,34 @@ __global__ __launch_bounds__(256) void k_filter_bits(const int64_t* __restrict__
   }
 }
 
+// The same bitmap from the whole filter index (KGE_RANK_FILTER_TABLE): one
+// wave per query looks its key's range up in the dense start table and sets
+// the bits of that range's ids (and the true id's)
+__global__ __launch_bounds__(256) void k_filter_bits_tab(const int64_t* __restrict__ queries, int head,
+                                                         const int64_t* __restrict__ tab,
+                                                         const int64_t* __restrict__ vals,
+                                                         const int64_t* __restrict__ true_id, int64_t nq, int64_t E,
+                                                         int64_t R, int64_t W, uint32_t* __restrict__ bits,
+                                                         int32_t* err) {
+  const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (q >= nq) return;
+  const int64_t t = true_id[q];
+  if (lane == 0 && t >= 0 && t < E) atomicOr(&bits[q * W + (t >> 5)], 1u << (t & 31));
+  const int64_t h = queries[q * 3], r = queries[q * 3 + 1], tl = queries[q * 3 + 2];
+  if (h < 0 || h >= E || tl < 0 || tl >= E || r < 0 || r >= R) return;  // (k_rank_prep flags bad ids)
+  const int64_t key = head ? r * E + tl : h * R + r;
+  const int64_t b = tab[key], e_ = tab[key + 1];
+  for (int64_t p = b + lane; p < e_; p += 64) {
+    const int64_t e = vals[p];
+    if (e < 0 || e >= E) {
+      atomicOr(err, KGE_DEVERR_INDEX);
+      continue;
+    }
+    atomicOr(&bits[q * W + (e >> 5)], 1u << (e & 31));
+  }
+}
+
 // rank = 1 + #{strictly greater} (counted beyond the window + refined inside
 // it), or the exact rescan's count for an overflowed window
 __global__ __launch_bounds__(256) void k_rank_emit(EmitArgs a) {
@@ -935,6 +963,17 @@ int launch_filter_bits(const int64_t* filt_off, const int64_t* filt_ids, const i
   if (nq > 65535) return -1;
   hipLaunchKernelGGL(k_filter_bits, dim3(4, (unsigned)nq), dim3(256), 0, s, filt_off, filt_ids, true_id, nq, E, W,
                      bits, err);
+  return (int)hipGetLastError();
+}
+
+int launch_filter_bits_tab(const int64_t* queries, int head, const int64_t* tab, const int64_t* vals,
+                           const int64_t* true_id, int64_t nq, int64_t E, int64_t R, uint32_t* bits, int32_t* err,
+                           hipStream_t s) {
+  const int64_t W = (E + 31) / 32;
+  hipError_t he = hipMemsetAsync(bits, 0, (size_t)nq * W * 4, s);
+  if (he != hipSuccess) return (int)he;
+  hipLaunchKernelGGL(k_filter_bits_tab, dim3((unsigned)((nq + 3) / 4)), dim3(256), 0, s, queries, head, tab, vals,
+                     true_id, nq, E, R, W, bits, err);
   return (int)hipGetLastError();
 }
 

@@ -57,6 +57,29 @@ class FilterIndex:
         hi[o] = np.searchsorted(cand, ks, side='right')
         return lo, hi
 
+    def device_table(self, mode: str, dev):
+        """(start table [E·R + 1], ids) int64 on `dev` for KGE_RANK_FILTER_TABLE:
+        key h·R + r → the true tails (tail-batch), r·E + t → the true heads
+        (head-batch), sorted by key; None when the index is too large for a
+        dense table (filter_csr then).  Cached per device."""
+        if self.nentity * self.nrelation > self.DENSE_KEYS:
+            return None
+        cache = self.__dict__.setdefault('_dev_tables', {})
+        k = (mode, str(dev))
+        if k not in cache:
+            import torch
+            if mode == 'tail-batch':
+                cand, vals, tag = self._k_hr, self._tails, '_tab_hr'
+            elif mode == 'head-batch':
+                cand, vals, tag = self._k_rt, self._heads, '_tab_rt'
+            else:
+                raise ValueError('negative batch mode %s not supported' % mode)
+            self._range(cand, np.zeros(1, dtype=np.int64), tag)  # builds the dense start table
+            tab = getattr(self, tag)
+            cache[k] = (torch.from_numpy(tab.astype(np.int64)).to(dev),
+                        torch.from_numpy(np.ascontiguousarray(vals, dtype=np.int64)).to(dev))
+        return cache[k]
+
     def filter_csr(self, queries, mode: str):
         """(offsets [nq+1] int64, ids int64) of the filtered candidates per query."""
         q = np.asarray(queries, dtype=np.int64).reshape(-1, 3)

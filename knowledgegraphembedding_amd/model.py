@@ -17,6 +17,7 @@ tensors are rejected instead of silently falling back.
 from __future__ import annotations
 
 import logging
+import os
 import time
 
 import numpy as np
@@ -574,6 +575,16 @@ class KGEModel(nn.Module):
             trig = self._rank_rotation(dev, relation_trig)
             qd = None
             for mode in ('head-batch', 'tail-batch'):
+                # a dense filter index is looked up on the device
+                # (KGE_RANK_FILTER_TABLE, uploaded once per index)
+                table = index.device_table(mode, dev) if os.environ.get("KGE_RANK_FILTER_TABLE", "1") != "0" else None
+                if table is not None:
+                    if qd is None:
+                        qd = torch.from_numpy(np.ascontiguousarray(q)).pin_memory().to(dev, non_blocking=True)
+                    outs.append(ops.rank_filtered(self.desc(), mode, qd, table[0], table[1], dev, path=path,
+                                                  relation_trig=trig, reuse_table=bool(outs),
+                                                  library_sin=self._rank_library_sin(), filter_table=True))
+                    continue
                 # the direction's inputs in one pinned host buffer, copied
                 # asynchronously: the tail's filter CSR is built on the host
                 # while the head direction's kernels run, and its copy queues

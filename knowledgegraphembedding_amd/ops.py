@@ -421,7 +421,7 @@ RANK_REUSE_TABLE = 0x100  # kge_hip.h KGE_RANK_REUSE_TABLE
 def rank_filtered(desc: _lib.ModelDesc, mode: str, queries: torch.Tensor, filt_off: torch.Tensor,
                   filt_ids: torch.Tensor, dev, path: str = "auto", listed: bool = False,
                   relation_trig: Optional[torch.Tensor] = None, reuse_table: bool = False,
-                  library_sin: bool = False):
+                  library_sin: bool = False, filter_table: bool = False):
     """Filtered ranks (int64) and tie counts (int32) for a block of queries
     (model.py:383-418), in the reference's fp32 score order
     (kge_rank_filtered_ex).  `path` picks the fast counting pass ("auto",
@@ -435,7 +435,10 @@ def rank_filtered(desc: _lib.ModelDesc, mode: str, queries: torch.Tensor, filt_o
     shared workspace is still the same buffer (else recomputed).
     `library_sin` (pRotatE): evaluate the sin of the near-ties' phase sums
     with the reference's own torch.sin on the host (reference_sin), so the
-    ranks are the reference's bit for bit; False: correctly rounded device sin."""
+    ranks are the reference's bit for bit; False: correctly rounded device sin.
+    `filter_table`: filt_off / filt_ids are the whole filter index
+    (FilterIndex.device_table: dense key → start table and the sorted ids)
+    instead of per-query lists; the device looks each query's list up."""
     if mode not in ("head-batch", "tail-batch"):
         raise ValueError("mode %s not supported" % mode)
     if path not in RANK_PATHS:
@@ -464,7 +467,7 @@ def rank_filtered(desc: _lib.ModelDesc, mode: str, queries: torch.Tensor, filt_o
     # (the library also checks its own tag of what the buffer holds)
     reuse_table = reuse_table and prev == (ws.data_ptr(),) + key
     st.rank_ws_ptr = (ws.data_ptr(),) + key
-    flags = RANK_PATHS[path] | (RANK_REUSE_TABLE if reuse_table else 0)
+    flags = RANK_PATHS[path] | (RANK_REUSE_TABLE if reuse_table else 0) | (_lib.RANK_FILTER_TABLE if filter_table else 0)
     mode_id = _lib.MODE_IDS[mode]
     if library_sin and desc.model == _lib.MODEL_IDS["pRotatE"] and nq:
         _rank_protate_library_sin(lib, desc, mode_id, q, nq, off, ids, ranks, ties, lst, flags, ws, st, dev)

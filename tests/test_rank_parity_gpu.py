@@ -373,3 +373,30 @@ def test_split_bf16_tile_wide_dynamic_range(name, wm, monkeypatch):
         r0, t0 = m.rank_queries(q, true, mode, path="scan")
         r1, t1 = m.rank_queries(q, true, mode, path="auto")
         assert np.array_equal(r0, r1) and np.array_equal(t0, t1), (name, mode)
+
+
+@pytest.mark.parametrize("name", ["DistMult", "ComplEx", "RotatE", "TransE"])
+def test_filter_table_matches_query_lists(name, monkeypatch):
+    """KGE_RANK_FILTER_TABLE (rank_queries_both's default for a dense filter
+    index: the device looks each query's filtered ids up in the whole index)
+    gives the ranks and ties of per-query filter lists built on the host
+    (rank_queries), on a wn18rr-shaped synthetic graph with repeated keys."""
+    from knowledgegraphembedding_amd import synth
+    from knowledgegraphembedding_amd.filters import FilterIndex
+    E, R, d = 3000, 11, 64
+    h, r, t = synth.randint(911, (20000,), E), synth.randint(912, (20000,), R), synth.randint(913, (20000,), E)
+    true = np.unique(np.stack([h, r, t], 1), axis=0)
+    test = true[synth.randint(914, (700,), len(true))]
+    index = FilterIndex(true, E, R)
+    cplx = name in ("ComplEx", "RotatE")
+    torch.manual_seed(3)
+    m = KGEModel(name, E, R, d, 12.0, cplx, name == "ComplEx").to(DEV)
+    (rh, th), (rt, tt) = m.rank_queries_both(test, index)
+    assert index.device_table("head-batch", DEV) is not None
+    ref_h = m.rank_queries(test, index, "head-batch")
+    ref_t = m.rank_queries(test, index, "tail-batch")
+    assert np.array_equal(rh, ref_h[0]) and np.array_equal(th, ref_h[1])
+    assert np.array_equal(rt, ref_t[0]) and np.array_equal(tt, ref_t[1])
+    monkeypatch.setenv("KGE_RANK_FILTER_TABLE", "0")
+    (rh2, th2), (rt2, tt2) = m.rank_queries_both(test, index)
+    assert np.array_equal(rh2, rh) and np.array_equal(rt2, rt) and np.array_equal(th2, th) and np.array_equal(tt2, tt)
