@@ -201,3 +201,26 @@ def test_run_main_requires_mode_and_paths():
         run.main(run.parse_args(["--do_test"]))
     with pytest.raises(ValueError, match="Where do you want to save your trained model"):
         run.main(run.parse_args(["--do_train", "--data_path", "x"]))
+
+
+def test_filter_device_table_matches_filter_csr():
+    """FilterIndex.device_table (the whole dense index KGE_RANK_FILTER_TABLE
+    passes to the device) holds, for every query key, the filter_csr list plus
+    the true entity itself (which the bitmap excludes anyway)."""
+    from knowledgegraphembedding_amd import synth
+    from knowledgegraphembedding_amd.filters import FilterIndex
+    E, R = 500, 7
+    h, r, t = synth.randint(21, (4000,), E), synth.randint(22, (4000,), R), synth.randint(23, (4000,), E)
+    true = np.unique(np.stack([h, r, t], 1), axis=0)
+    q = true[synth.randint(24, (300,), len(true))]
+    index = FilterIndex(true, E, R)
+    for mode in ("head-batch", "tail-batch"):
+        tab, vals = index.device_table(mode, "cpu")
+        tab, vals = tab.numpy(), vals.numpy()
+        assert tab.shape == (E * R + 1,)
+        off, ids = index.filter_csr(q, mode)
+        for i, (hh, rr, tt) in enumerate(q):
+            key = rr * E + tt if mode == "head-batch" else hh * R + rr
+            got = set(vals[tab[key]:tab[key + 1]].tolist())
+            want = set(ids[off[i]:off[i + 1]].tolist()) | {hh if mode == "head-batch" else tt}
+            assert got == want, (mode, i)
