@@ -170,13 +170,14 @@ def host_cores() -> int:
     return n
 
 
-def cpu_baseline(model_cpu_state, budget_s: float = 30.0, b: int = B, max_steps: int = 2):
+def cpu_baseline(model_cpu_state, budget_s: float = 90.0, b: int = B, max_steps: int = 2):
     """The oracle (the reference's ATen op chain on CPU fp32 + torch.optim.Adam)
     on the workload itself — BASELINE config 2's full b = 1024 × n = 256 step
      — on every host core this process may run on: one small
     warm-up step (b = 16: thread pool and allocator), then full-batch steps,
     tail- then head-batch, until `max_steps` are timed or `budget_s` has
-    passed after the first (a full step takes ≈ 20-40 s on 8-16 cores)."""
+    passed after the first (a full step takes ≈ 20-45 s on 8-16 cores, so the
+    default budget times two)."""
     from oracle import kge_oracle as O
     ent, rel, erange = model_cpu_state
     cores = host_cores()
@@ -268,6 +269,104 @@ def rank_section(dev, reps: int = 3) -> dict:
                      "mrr": float(np.mean(1.0 / np.concatenate([rh, rt])))}
         del m
     torch.cuda.empty_cache()
+    out.update(distance_rank_section(dev, reps))
+    return out
+
+
+# VALU issue bound of the register tile (k_rank_tile) per pair-element —
+# one reduction element of one (query, candidate) pair — from its inner loop's
+# instruction mix: issue cycles per wave for 64 pair-elements, at
+# 4 SIMDs × 256 CUs × 2.4 GHz.
+TILE_ISSUE_CYC = {"RotatE": 22.0, "TransE": 8.0, "pRotatE": 12.0}
+
+
+def _rank_timer_read(lib):
+    import ctypes
+    import numpy as np
+    buf = np.zeros(4, dtype=np.float32)
+    _lib.check(lib.kge_stage_timer(5, buf.ctypes.data_as(ctypes.c_void_p), 4), "kge_stage_timer")
+    return buf
+
+
+def distance_rank_section(dev, reps: int = 3) -> dict:
+    """The distance models' filtered ranking — the register-tile streaming scan
+    (k_rank_tile) + near-tie refinement — measured live: RotatE and TransE at
+    the FB15k shape best_config.sh:3 / :27 evaluate (E=14951, R=1345, d=1000,
+    γ=24; 4096 test triples × both directions against a synthetic filter graph
+    of FB15k's 592,213 true triples), pRotatE at the wn18rr shape (E=40943,
+    R=11, d=500, γ=6; 3134 × 2 queries, the config-3 graph) with the
+    reference's own host sin for its near-ties (ranks bit-exact, three-call
+    form).  Per model: the whole pass's wall time and queries/s, and from the
+    ranking timer (HIP events on the launch stream, kge_stage_timer 4/5) the
+    fast pass's average launch time per direction → pair-element terms/s
+    against the tile's VALU issue bound, and the bytes the tile streams from
+    L2 / Infinity Cache (every query tile of 64 reads the whole table, every
+    candidate tile the query block) over that time."""
+    import numpy as np
+    from knowledgegraphembedding_amd import synth
+    from knowledgegraphembedding_amd.filters import FilterIndex
+    lib = _lib.load()
+    cases = []
+    # FB15k shape: train + valid + test = 592,213 triples (483,142 + 50,000 + 59,071)
+    Ef, Rf, nq_f = 14951, 1345, 4096
+    tf = np.unique(np.stack([synth.randint(911, (592213,), Ef), synth.randint(912, (592213,), Rf),
+                             synth.randint(913, (592213,), Ef)], 1), axis=0)
+    test_f = tf[synth.randint(914, (nq_f,), len(tf))]
+    idx_f = FilterIndex(tf, Ef, Rf)
+    cases.append(("RotatE", True, False, 1000, 24.0, Ef, Rf, test_f, idx_f, "FB15k"))
+    cases.append(("TransE", False, False, 1000, 24.0, Ef, Rf, test_f, idx_f, "FB15k"))
+    Ew, Rw, ntest = 40943, 11, 3134
+    tw = np.unique(np.stack([synth.randint(901, (93003,), Ew), synth.randint(902, (93003,), Rw),
+                             synth.randint(903, (93003,), Ew)], 1), axis=0)
+    test_w = tw[synth.randint(904, (ntest,), len(tw))]
+    cases.append(("pRotatE", False, False, 500, 6.0, Ew, Rw, test_w, FilterIndex(tw, Ew, Rw), "wn18rr"))
+    out = {}
+    for name, de, dr, d, gamma, En, Rn, test, index, shape in cases:
+        torch.manual_seed(0)
+        m = KGEModel(name, En, Rn, d, gamma, de, dr).to(dev)
+        m.rank_trig = "reference"
+        nq = 2 * len(test)
+        best, stages = None, None
+        for rep in range(reps + 1):
+            if rep == 1:
+                _lib.check(lib.kge_stage_timer(4, None, 0), "kge_stage_timer")  # warm-up pass untimed
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            (rh, _), (rt, _) = m.rank_queries_both(test, index)
+            torch.cuda.synchronize()
+            dt = time.perf_counter() - t0
+            if rep and (best is None or dt < best):
+                best = dt
+        stages = _rank_timer_read(lib)
+        lib.kge_stage_timer(0, None, 0)
+        calls = max(1.0, float(stages[3]))
+        fast_ms = float(stages[1]) / calls
+        Kred = d  # reduction length per pair: complex dims (RotatE) or floats (TransE, pRotatE)
+        Le = m.entity_dim
+        terms = (nq / 2) * En * Kred  # one direction per call
+        bound = 4 * 256 * 2.4e9 * 64 / TILE_ISSUE_CYC[name]
+        tiles_q, tiles_e = -(-(nq // 2) // 64), -(-En // 64)
+        streamed = 4.0 * Le * (tiles_q * En + tiles_e * (nq // 2))
+        out[name] = {
+            "shape": f"{shape} E={En} R={Rn} d={d} (entity_dim {Le}), {nq} queries (both directions), "
+                     f"synthetic filter graph, rank_trig=reference",
+            "ms": best * 1e3, "queries_per_s": nq / best,
+            "fast_pass_ms_per_direction": fast_ms,
+            "prep_ms_per_direction": float(stages[0]) / calls,
+            "refine_ms_per_direction": float(stages[2]) / calls,
+            "timed_calls": int(stages[3]),
+            "valu": {"bound": "valu", "achieved_terms_per_s": terms / (fast_ms * 1e-3),
+                     "peak_terms_per_s": bound, "frac": terms / (fast_ms * 1e-3) / bound,
+                     "issue_cycles_per_wave_per_64_terms": TILE_ISSUE_CYC[name],
+                     "what": "pair-element terms (query × candidate × reduction element) per second of the "
+                             "register tile against its VALU issue bound (DESIGN §5)"},
+            "streamed": {"bytes_per_direction": streamed, "achieved_GBps": streamed / (fast_ms * 1e-3) / 1e9,
+                         "what": "table + query bytes the tile reads from L2 / Infinity Cache per launch "
+                                 "(64-query × 64-candidate tiles) over its launch time; HBM: the table once"},
+            "mrr": float(np.mean(1.0 / np.concatenate([rh, rt]))),
+        }
+        del m
+    torch.cuda.empty_cache()
     return out
 
 
@@ -277,7 +376,8 @@ def main():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-budget", type=float, default=30.0)
+    ap.add_argument("--cpu-budget", type=float, default=90.0,
+                    help="seconds after which no further full CPU step starts (two are timed when the first ends sooner)")
     ap.add_argument("--no-stage-timer", action="store_true",
                     help="skip the per-stage HIP events (roofline then comes from the committed rocprof summary)")
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="fb15k")

@@ -498,9 +498,21 @@ int kge_rank_finish_sin(const kge_model_desc *m, int32_t mode, int64_t nq, const
  *   command 3: the same per timed call: stage_ms_out[7c .. 7c+5] the call's
  *              stage times, stage_ms_out[7c+6] its start (ms after the first
  *              timed call's start); n_out >= 7 × timed calls.
+ *   command 4: enable and reset the RANKING timer: every kge_rank_filtered* call
+ *              (and pRotatE's three-call form, list → finish) records events
+ *              at its start, around its fast counting pass and after its ranks
+ *              are written (command 0 disables it too);
+ *   command 5: synchronise them and write the summed milliseconds of its
+ *              KGE_RANK_TIMER_STAGES stages — 0 query / filter / table
+ *              preparation and windows, 1 the fast counting pass (MFMA tile,
+ *              register tile or wave scan), 2 near-tie refinement and rank
+ *              emission (pRotatE's three-call form: including the caller's
+ *              host sin between the calls) — then the number of calls
+ *              (n_out >= 4).
  * Not graph-capturable while enabled.
  */
 #define KGE_TIMER_STAGES 6
+#define KGE_RANK_TIMER_STAGES 3
 int kge_stage_timer(int32_t command, float *stage_ms_out, int32_t n_out);
 
 /*

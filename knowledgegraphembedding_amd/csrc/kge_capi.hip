@@ -114,7 +114,6 @@ struct Carver {
 struct GradWs {
   float *g, *q, *dq, *ent_contrib, *rel_contrib, *row_stats, *reg_partial, *wsum;
   int32_t *keys, *cnt, *off, *tmp, *occ;
-  int32_t *bkt, *bkt_cnt;  // occurrence buckets [E, BKT_CAP] + counts [E] (the single-call step)
   float* q_sl;  // slice-major q for the sliced entity pass (KGE_ENT_QSL)
   void* scan_tmp;
   size_t scan_tmp_bytes;
@@ -138,8 +137,6 @@ GradWs carve_grad(void* ws, const kge_model_desc* m, int64_t B, int64_t n, size_
   w.tmp = c.take<int32_t>(N);
   w.occ = c.take<int32_t>(N);
   w.q_sl = c.take<float>(8 * B * 512);  // up to 8 slices × B rows × (64 + 64) float4 slots
-  w.bkt = c.take<int32_t>(m->nentity * (int64_t)BKT_CAP);
-  w.bkt_cnt = c.take<int32_t>(m->nentity);
   w.scan_tmp_bytes = csr_scan_temp_bytes(nb);
   w.scan_tmp = c.take<uint8_t>((int64_t)w.scan_tmp_bytes);
   *bytes = c.off + 256;
@@ -163,11 +160,6 @@ struct StageTimer {
     }
     return ev[used++];
   }
-  hipEvent_t dbg = nullptr;
-  void marker(hipStream_t s) {  // KGE_DBG_EVENTS: an untimed event record, as the side-stream fork is
-    if (!dbg && hipEventCreateWithFlags(&dbg, hipEventDisableTiming) != hipSuccess) return;
-    hipEventRecord(dbg, s);
-  }
   void mark(hipStream_t s) {
     if (!on) return;
     hipEvent_t e = next(s);
@@ -176,6 +168,9 @@ struct StageTimer {
 };
 StageTimer g_timer;
 void timer_mark(hipStream_t s) { g_timer.mark(s); }
+// the ranking's stage timer (kge_stage_timer commands 4 / 5): KGE_RANK_TIMER_STAGES + 1
+// events per ranking call — start, fast pass begin, fast pass end, ranks written
+StageTimer g_rank_timer;
 
 // ---- side stream: the index-only work (occurrence CSR) and the relation
 // pass run beside the gather kernels of the caller's stream.  Fork/join via
@@ -185,6 +180,12 @@ struct Side {
   hipStream_t s = nullptr;
   hipEvent_t fork = nullptr, csr_done = nullptr, epi_done = nullptr, rel_done = nullptr;
 };
+// Diagnostic switches, read per call so a test can flip them between calls;
+// none changes a result bit (each selects between paths that are tested
+// bitwise equal): KGE_ENT_SLICES (force the entity pass's column-slice count;
+// 0 = the row-per-wave k_entity), KGE_FIN_SEPARATE (the loss finalisation as
+// its own launch), KGE_RANK_SIN_SCREEN=0 (pRotatE: send every listed
+// near-tie to the caller's sin, no device screen).
 int env_int(const char* name, int dflt) {
   const char* e = getenv(name);
   return e ? atoi(e) : dflt;
@@ -239,7 +240,7 @@ int entity_slices(const Geom& geo, int64_t B, int Le) {
 // phase is one the 64-slot slices absorb (last slice ≤ 64 slots) — d = 1000:
 // phases 0 and 4 — and KGE_ENT_ALIGN is not 0.
 int entity_slice_align(int nsl, int S, int Le, const float* ent, const float* grad, const AdamT& ad) {
-  if (nsl < 2 || env_int("KGE_ENT_ALIGN", 1) == 0) return 0;
+  if (nsl < 2) return 0;
   const uintptr_t base = (uintptr_t)ent & 127;
   if (base & 15) return 0;
   for (const float* p : {grad, (const float*)ad.p, (const float*)ad.m, (const float*)ad.v})
@@ -302,31 +303,18 @@ int run_grad(const kge_model_desc* m, const Geom& geo, int mode, const int64_t* 
   // no stream join); else beside the entity pass on the side stream (always
   // so in phased calls)
   const bool rel_fused = all && nsl > 0;
-  // slice-major q (KGE_ENT_QSL, default on): k_row also writes q as
-  // [slice][row][re | im] so each of the entity pass's q reads is 2 KB
-  // contiguous and line-aligned (0.240 -> 0.234 ms at the FB15k shape); the
-  // single-call step with even slices only (the line-aligned slices shift a
-  // row's columns by its phase, so they are off here)
+  // slice-major q: k_row also writes q as [slice][row][re | im] so each of
+  // the entity pass's q reads is 2 KB contiguous and line-aligned (0.240 ->
+  // 0.234 ms at the FB15k shape); the single-call step with even slices only
+  // (the line-aligned slices shift a row's columns by its phase, so they are
+  // off here)
   const bool q_slm = all && nsl > 0 && geo.vec == 4 && xstage == XS_NONE && ra.op == ROW_TRAIN &&
-                     (geo.eg.S + nsl - 1) / nsl <= 64 && env_int("KGE_ENT_QSL", 1) != 0 &&
-                     env_int("KGE_ENT_DMA", 0) == 0;
+                     (geo.eg.S + nsl - 1) / nsl <= 64;
   ra.q_sl = q_slm ? w.q_sl : nullptr;
   ra.q_sl_w = q_slm ? (geo.eg.S + nsl - 1) / nsl : 0;
   const bool rel_side = sd && !rel_fused;
-  // occurrence buckets filled by k_row instead of the CSR (KGE_ENT_BUCKETS=1;
-  // bit-identical): the single-call step on the slice-major path, when the
-  // average bucket is far below its capacity (an overflowed bucket is still
-  // exact, only slow).  No side stream: no fork marker, no join, nothing
-  // beside k_row.  Off by default: it saves the ≈6.5 µs join but the entity
-  // pass pays ≈8-9 µs for the per-wave sort and the bucket reads, ≈1.3 %
-  // per step net (profiles/r04/train/).
-  const bool buckets = q_slm && env_int("KGE_ENT_BUCKETS", 0) != 0 &&
-                       (double)B * (double)(n + 2) <= 32.0 * (double)m->nentity;
-  ra.bkt = buckets ? w.bkt : nullptr;
-  ra.bkt_cnt = buckets ? w.bkt_cnt : nullptr;
   RelArgs rl;
   memset(&rl, 0, sizeof(rl));
-  rl.pos = buckets ? pos : nullptr;
   rl.rel = m->relation_embedding; rl.R = m->nrelation; rl.E = m->nentity; rl.B = B; rl.Bn = B * n; rl.Lr = Lr;
   rl.off = w.off; rl.occ = w.occ; rl.rel_contrib = w.rel_contrib; rl.reg3 = 3.f * reg;
   rl.reg_partial = w.reg_partial + ent_parts; rl.grad_rel = grad_relation;
@@ -354,16 +342,12 @@ int run_grad(const kge_model_desc* m, const Geom& geo, int mode, const int64_t* 
   if (xstage == XS_CSR_ONLY) return launch_status(launch_csr(ca, s));  // kge_train_csr
   if (from_rows) ra.fuse_epi = 0;  // the epilogue reads the gathered dL/dq (k_row_epi)
 
-  const bool use_csr = !csr_ready && !buckets;
+  const bool use_csr = !csr_ready;
   if (phases & KGE_PHASE_ROWS) {
   // fork point: the occurrence CSR needs only the batch indices (recorded
   // before anything else is queued, so the side stream never waits for the
   // row pass)
   if (sd && use_csr) hipEventRecord(sd->fork, s);
-  if (buckets) {  // k_row's atomics count from zero
-    const hipError_t me = hipMemsetAsync(w.bkt_cnt, 0, sizeof(int32_t) * (size_t)m->nentity, s);
-    if (me != hipSuccess) return hip_status(me);
-  }
 
   // q build + gather loop on the caller's stream, launched first so the GPU
   // is on the long kernel while the host queues everything else
@@ -438,15 +422,10 @@ int run_grad(const kge_model_desc* m, const Geom& geo, int mode, const int64_t* 
   ea.write_grad = write_grad;
   ea.nsl = nsl;
   ea.slice_w = nsl > 0 ? (geo.eg.S + nsl - 1) / nsl : 0;
-  ea.dma = (nsl > 0 && (double)B * Le * 4.0 < 2147483648.0 && env_int("KGE_ENT_DMA", 0) != 0) ? 1 : 0;
-  ea.variant = env_int("KGE_ENT_VARIANT", 0);
   ea.adam = adam_t(adam ? &adam->entity : nullptr);
   ea.adamk = ak;
   ea.align_sl = q_slm ? 0 : entity_slice_align(nsl, geo.eg.S, Le, m->entity_embedding, write_grad ? grad_entity : nullptr, ea.adam);
   ea.q_sl = q_slm ? w.q_sl : nullptr;
-  ea.bkt = buckets ? w.bkt : nullptr;
-  ea.bkt_cnt = buckets ? w.bkt_cnt : nullptr;
-  ea.pos = pos; ea.neg = neg; ea.neg_stride = neg_stride;
   ea.rel = rl;
   ea.B = B;
   ea.rel_blocks = rel_fused ? (m->nrelation + 3) / 4 : 0;
@@ -471,7 +450,6 @@ int run_grad(const kge_model_desc* m, const Geom& geo, int mode, const int64_t* 
     st = launch_status(launch_rel_rows(rl, s));
     if (st) return st;
   }
-  for (int k = env_int("KGE_DBG_EVENTS", 0); k > 0; --k) g_timer.marker(s);  // diagnostic: cost of a marker
   if (fin_wanted && !fin_fused) {
     st = launch_status(launch_finalize(fa, s));
     if (st) return st;
@@ -839,8 +817,6 @@ int kge_ship_step(const kge_model_desc* m, int32_t mode, const kge_ship_desc* sh
   ea.write_grad = (!adam || adam->write_grad) ? 1 : 0;
   ea.nsl = nsl;
   ea.slice_w = nsl > 0 ? (geo.eg.S + nsl - 1) / nsl : 0;
-  ea.dma = (nsl > 0 && (double)B * Le * 4.0 < 2147483648.0 && env_int("KGE_ENT_DMA", 0) != 0) ? 1 : 0;
-  ea.variant = env_int("KGE_ENT_VARIANT", 0);
   ea.adam = adam_t(adam ? &adam->entity : nullptr);
   ea.adamk = ak;
   ea.B = B;
@@ -1077,22 +1053,18 @@ int rank_impl(const kge_model_desc* m, int32_t mode, const int64_t* queries, int
   ra.trig = trig;
   ra.item_off = item_off; ra.sins = sins; ra.args = args;
   ra.lib_sin = (stage != RS_ALL) ? 1 : 0;
-  // the split-bf16 tile's error bound in units of u·‖q‖·max‖e‖ (kge_rank_mfma.hip)
+  // the split-bf16 tile's error bound in units of u·‖q‖·max‖e‖ (kge_rank_mfma.hip): splitting
+  // residuals and the final add 513.2, the dropped lo·lo products 256·(1 + 2^-8)^2 = 258.1, the
+  // slab's three chained MFMAs 97.6, the running sum 1.02·nslab
   const int64_t xns = xsplit_nslab(m->entity_dim);
-  // the split tile's bound in u·‖q‖·max‖e‖ (kge_rank_mfma.hip): splitting 512.1, hi·hi MFMAs 32.3, running
-  // sum 1.02·nslab, correction chain 0.0472·Kp, final add 1.01 (+64.2 with the lo·lo products dropped);
-  // KGE_XTILE_MERGE: the corrections inside each slab's hi·hi chain, 3 (4) chained MFMAs of ≤ 32u
-  // each on partial sums ≤ (1 + 2^-8)·P_slab: 96.5 (128.5) in place of 32.3 + 0.0472·Kp
-  const bool lolo = xsplit_lolo();
-  ra.fast_u = (rp != RP_MFMA) ? 0.f
-              : xsplit_merge() ? (float)(513.2 + (lolo ? 128.5 : 96.5) + 1.02 * xns + (lolo ? 0.0 : 64.2))
-                               : (float)(546.0 + 1.02 * xns + 0.05 * xns * 16 + (lolo ? 0.0 : 64.2));
+  ra.fast_u = (rp != RP_MFMA) ? 0.f : (float)(513.2 + 258.1 + 97.6 + 1.02 * xns);
   if (stage == RS_ARGS) return launch_status(ops.rank_ref(mode, 3, ra, s));
   EmitArgs ea;
   ea.gt = w.gt; ea.eq = w.eq; ea.gtx = w.gtx; ea.eqx = w.eqx; ea.ucnt = w.ucnt; ea.true_id = w.true_id;
   ea.nq = nq; ea.cap = RANK_CAP; ea.ranks = ranks_out; ea.ties = ties_out; ea.listed = listed_out;
 
   if (stage != RS_FINISH) {
+    g_rank_timer.mark(s);  // (rank timer) 0: the call starts
     st = launch_status(ops.rank(mode, geo.vec, geo.ns, a, s));
     if (st) return st;
     // 2. excluded candidates (filtered ids + the true id) as a bitmap
@@ -1119,8 +1091,9 @@ int rank_impl(const kge_model_desc* m, int32_t mode, const int64_t* queries, int
     ta.c = a.c; ta.true_id = w.true_id; ta.s_true = w.s_true;
     ta.fbits = w.bits; ta.W = a.W; ta.gt = w.gt; ta.win = win;
     // split-bf16 path: s_true in the reference's order after the window
-    // (k_rank_true_ref, KGE_RANK_TRUE_REF=0: the gather-mode tile here)
-    const bool true_ref = rp == RP_MFMA && ((m->entity_dim + 3) & ~3) <= 1024 && env_int("KGE_RANK_TRUE_REF", 1) != 0;
+    // (k_rank_true_ref, rows of ≤ 1024 floats: its LDS); wider rows take the
+    // tile's own gather mode here (the window then covers two fast scores)
+    const bool true_ref = rp == RP_MFMA && ((m->entity_dim + 3) & ~3) <= 1024;
     if (rp == RP_MFMA) {
       st = launch_status(launch_split_bf16(w.q, nq, m->entity_dim, w.qs, s));
       if (!st)
@@ -1143,6 +1116,7 @@ int rank_impl(const kge_model_desc* m, int32_t mode, const int64_t* queries, int
       if (st) return st;
     }
     // 5. fast counting pass: clear cases counted, near-ties listed
+    g_rank_timer.mark(s);  // (rank timer) 1: fast pass begins
     if (rp == RP_MFMA) {
       st = launch_status(launch_rank_mfma_x(0, w.qs, w.es, nq, m->nentity, m->entity_dim, w.true_id, w.s_true,
                                             w.bits, w.gt, win, s));
@@ -1157,6 +1131,7 @@ int rank_impl(const kge_model_desc* m, int32_t mode, const int64_t* queries, int
       st = launch_status(ops.rank(mode, geo.vec, geo.ns, a, s));
     }
     if (st) return st;
+    g_rank_timer.mark(s);  // (rank timer) 2: fast pass ends
     if (stage == RS_LIST) {  // the lists stay in the workspace for RS_ARGS / RS_FINISH
       // pRotatE: the listed candidates re-scored with correctly rounded sin in
       // the reference's order; those the library sin cannot move past the true
@@ -1179,7 +1154,9 @@ int rank_impl(const kge_model_desc* m, int32_t mode, const int64_t* queries, int
   if (st) return st;
   st = launch_status(ops.rank_ref(mode, 2, ra, s));
   if (st) return st;
-  return launch_status(launch_rank_emit(ea, s));
+  st = launch_status(launch_rank_emit(ea, s));
+  if (!st) g_rank_timer.mark(s);  // (rank timer) 3: ranks written
+  return st;
 }
 }  // namespace
 }  // namespace kge
@@ -1222,6 +1199,34 @@ int kge_stage_timer(int32_t command, float* stage_ms_out, int32_t n_out) {
     g_timer.used = 0;
     g_timer.seen = 0;
     g_timer.period = (command == 1 && n_out > 0) ? n_out : 1;
+    if (command == 0) {
+      g_rank_timer.on = false;
+      g_rank_timer.used = 0;
+    }
+    return KGE_OK;
+  }
+  if (command == 4) {  // ranking calls: enable and reset
+    g_rank_timer.on = true;
+    g_rank_timer.used = 0;
+    return KGE_OK;
+  }
+  if (command == 5) {  // ranking calls: summed stage times + the number of calls
+    constexpr int NR = KGE_RANK_TIMER_STAGES + 1;
+    if (!stage_ms_out || n_out < NR) return KGE_ERR_ARG;
+    for (int k = 0; k < NR; ++k) stage_ms_out[k] = 0.f;
+    const size_t calls = g_rank_timer.used / NR;
+    for (size_t c = 0; c < calls; ++c) {
+      hipEvent_t* e = &g_rank_timer.ev[c * NR];
+      hipError_t err = hipEventSynchronize(e[NR - 1]);
+      if (err != hipSuccess) return hip_status(err);
+      for (int k = 0; k < KGE_RANK_TIMER_STAGES; ++k) {
+        float ms = 0.f;
+        err = hipEventElapsedTime(&ms, e[k], e[k + 1]);
+        if (err != hipSuccess) return hip_status(err);
+        stage_ms_out[k] += ms;
+      }
+    }
+    stage_ms_out[KGE_RANK_TIMER_STAGES] = (float)calls;
     return KGE_OK;
   }
   const size_t calls = g_timer.used / NS_;

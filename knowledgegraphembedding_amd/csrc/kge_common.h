@@ -27,10 +27,8 @@ int launch_rank_mfma(int gather, const float* q, const float* ent, int64_t nq, i
                      hipStream_t s);
 // split-bf16 MFMA tile (path "mfma"): operands split once per call into bf16 hi | lo pieces
 int64_t xsplit_nslab(int K);
-// the split tile's lo·lo products (KGE_XTILE_LOLO, default 0: dropped — three
-// MFMAs per product instead of four, +64.2·u·P on the error bound; 1 keeps them)
-bool xsplit_lolo();
-bool xsplit_merge();
+// (three bf16 MFMAs per fp32 product: the lo·lo products are dropped, +258.1·u·P
+// on the error bound — kge_rank_mfma.hip, kge_capi.hip rank_impl)
 int64_t xsplit_elems(int64_t rows, int K);
 int launch_split_bf16(const float* src, int64_t rows, int K, uint16_t* dst, hipStream_t s,
                       const int64_t* skip = nullptr);

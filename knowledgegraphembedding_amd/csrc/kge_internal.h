@@ -78,18 +78,7 @@ struct RowArgs {
   ShipArgs sh;        // query shipping stages only
   float* q_sl;        // non-null (VEC = 4): q also slice-major for k_entity_sl, [slice][row][re 64 | im 64 slots]
   int q_sl_w;         //   slots per slice
-  int32_t* bkt;       // non-null: occurrence buckets, filled in k_row's prologue (see OccBuckets)
-  int32_t* bkt_cnt;   //   [E] counts (zeroed before the launch)
 };
-
-// Fixed-capacity occurrence buckets (the single-call training step): k_row
-// appends each of its row's occurrence ids — negatives i·n + j, the row's
-// head / tail slots Bn + 2i / Bn + 2i + 1 — to bucket[entity] by one atomic
-// per occurrence; the entity pass sorts a bucket's ≤ BKT_CAP ids in registers
-// (ascending, the CSR's order) and, for an entity with more occurrences than
-// that, scans every occurrence of the batch in id order instead.  No CSR, no
-// side stream.
-constexpr int BKT_CAP = 64;
 
 // k_row's LDS merge buffer: [2][Le] floats, and at least the 256 floats the
 // fused Σw reduction (block_weight_sum) uses as its tree
@@ -101,7 +90,6 @@ struct RelArgs {
   int Lr;
   const int32_t* off;
   const int32_t* occ;
-  const int64_t* pos;        // non-null: no relation buckets — scan the batch's relation ids (ascending rows)
   const float* rel_contrib;  // [B, Lr]
   float reg3;
   float* reg_partial;        // [R]
@@ -153,13 +141,6 @@ struct EntArgs {
   int slice_w;
   int align_sl;         // k_entity_sl: line-aligned 64-slot slices per row (entity_slice_align)
   const float* q_sl;    // k_entity_sl<.., QSL>: q slice-major (written by k_row; even slices only) or null
-  int dma;              // k_entity_sl stages the q slices by LDS-DMA (needs B·Le·4 < 2^31)
-  int variant;          // k_entity_sl bucket path: 1 late moments, 2 eight q rows in flight, 3 both, 4 late + six, 5 wave-specialised (KGE_ENT_VARIANT)
-  const int32_t* bkt;   // k_entity_sl<.., BK>: occurrence buckets [E, BKT_CAP] (instead of off / occ)
-  const int32_t* bkt_cnt;  // [E]
-  const int64_t* pos;   // BK, an overflowed bucket: the batch's ids, scanned in occurrence order
-  const int64_t* neg;
-  int64_t neg_stride;
   AdamT adam;           // fused optimizer step (adam.p == null: none)
   AdamK adamk;
   RelArgs rel;          // rel_blocks > 0: trailing blocks of k_entity_sl run the relation pass

@@ -320,17 +320,20 @@ __global__ __launch_bounds__(256) void k_rank_emit(EmitArgs a) {
 // up to the near-tie window — the window's candidates are re-scored in the
 // reference's fp32 order anyway — so it may compute in any precision whose
 // error it bounds.  Each operand x is split as x = x_hi + x_lo + r with
-// x_hi = bf16(x), x_lo = bf16(x − x_hi) (both RNE, |r| ≤ 2^-16 |x|), and
-//   s ≈ Σ_slab fl(Σ_16 e_hi q_hi)  +  Σ_k (e_hi q_lo + e_lo q_hi + e_lo q_lo)
-// (bf16 × bf16 products are exact in fp32).  The hi·hi part of each 16-k
-// slab comes from an MFMA with a zero accumulator and is added to an fp32
-// running sum by v_add (rounded once per slab); the three small products
-// chain in a second accumulator.  Error per score, P = Σ|q_k||e_k| ≤ ‖q‖‖e‖:
-//   splitting 512.1·u·P, hi·hi MFMAs 32.3·u·P (2u per internal add, any
-//   order), running sum 1.02·nslab·u·P, correction chain 0.0472·Kp·u·P
-//   (3 Kp terms of total size ≤ 2^-7·P), final add 1.01·u·P
-// → (546 + 1.02·nslab + 0.05·Kp)·u·P (k_rank_window, xsplit = 1), about the
-// fp32 tile's K·u for K = 500 and below it for larger K.
+// x_hi = bf16(x), x_lo = bf16(x − x_hi), both round-to-nearest-even with 8
+// significant bits: |x − x_hi| ≤ 2^-8 |x|, |x_lo| ≤ 2^-8 (1 + 2^-8) |x|,
+// |r| ≤ 2^-16 |x|.  Per 16-k slab one MFMA chain computes e_hi·q_hi from a
+// zero accumulator, then adds e_hi·q_lo and e_lo·q_hi (bf16 × bf16 products
+// are exact in fp32); the chain's result joins an fp32 running sum (one
+// rounding per slab); e_lo·q_lo is never computed.  Error per score against
+// the exact Σ e_k q_k, u = 2^-24, P = Σ|q_k||e_k| ≤ ‖q‖‖e‖:
+//   splitting residuals      2·2^-16·P (+ the final add's 1.01·u·P) → 513.2·u·P
+//   the dropped lo·lo        2^-16 (1 + 2^-8)^2·P                   → 258.1·u·P
+//   the three chained MFMAs  ≤ 32·u each on partial sums ≤ (1 + 2^-8)^2 (1 + 2^-7)·P_slab
+//                            (2u per internal add, any order)      →  97.6·u·P
+//   the running sum          1.02·nslab·u·P
+// → fast_u = (868.9 + 1.02·nslab)·u·P (kge_capi.hip rank_impl, RefArgs.fast_u;
+// the window k_rank_window sizes from it), against the fp32 tile's K·u.
 //
 // Operands are split once per call into a tile-linear layout
 // [row block of 128][16-k slab][hi | lo][128 rows][16 k] bf16 (k_split_bf16),
@@ -341,13 +344,11 @@ __global__ __launch_bounds__(256) void k_rank_emit(EmitArgs a) {
 // two lanes on every bank quad of a group they use (2-way conflicts, half
 // the banks idle: SQ_LDS_BANK_CONFLICT ≈ the LDS-active cycles); with the
 // swap each group's 16 lanes cover all 64 banks.  Rows past nq / E and k ≥ K are
-// zeros in the split buffers.  256 threads as 2×2 waves of 64×64 (2×2 MFMA
-// tiles), 4-stage LDS ring (64 KB) with 3 slabs in flight, 2 workgroups per CU.
+// zeros in the split buffers.
 typedef short bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 constexpr int XS_BK = 16;                   // k per slab = one 32x32x16 MFMA step
 constexpr int XS_PIECE = 128 * XS_BK;       // bf16 per (row block, slab, hi|lo) = 4 KB
-constexpr int XS_NST = 4;                   // LDS ring stages
 constexpr uint32_t XS_OOB = 0x7FFFFFF0u;
 
 __device__ __forceinline__ uint32_t bf16_rne(float x) {
@@ -432,56 +433,40 @@ __device__ __forceinline__ bool xcd_tile(const XArgs& a, int& x, int& y) {
   return true;
 }
 
-// TQ = query column tiles (32 each) per wave: a workgroup is 2 × 2 waves
-// over 128 candidates × 64·TQ queries.  TQ = 2 (default): 64×64 per wave,
-// 239 VGPRs, 64 KB ring, 2 workgroups per CU.  TQ = 1 (KGE_XTILE_TQ=1): 64×32
-// per wave, 133 VGPRs, a 48 KB ring, 3 workgroups per CU — more waves per SIMD
-// for 1.5× the fragment reads per MFMA and twice the candidate-tile DMAs;
-// measured equal (530 vs 523 µs, profiles/r03/rank/ab_tile_variants.txt).
-// (Timing diagnostics that dropped the MFMAs, the LDS-DMA or the epilogue —
-// measurements in profiles/r03/rank/ab_tile_variants.txt — are not in the tree.)
-// WM = waves along the candidates: 2 (128 candidates per workgroup, 256
-// threads, 2 workgroups per CU) or 4 (256 candidates, 512 threads, one
-// workgroup per CU: the same 64×64 per wave, a third less L2 → LDS traffic
-// per MFMA — each slab's query piece feeds twice the candidates).
-// s_waitcnt vmcnt(n) for the DMA counts the ring loops need (n = slabs × CPW
-// with CPW 3 or 4 and ≤ 4 younger slabs); any other n waits for everything
+// The counting tile: 256 threads as 2 × 2 waves over 128 candidates × 128
+// queries, 64 × 64 per wave (2 × 2 blocks of 32 × 32), a 3-stage LDS ring
+// (two slabs in flight), three workgroups per CU (≈170 VGPRs).  Per 16-k slab
+// and 32 × 32 block, hi·hi starts a fresh MFMA chain (zero accumulator) and
+// the hi·lo and lo·hi products chain onto it; the chain's result is added to
+// the fp32 running sum one slab later (so no add waits on its MFMA).  The lo·lo
+// product is not computed: its |e_lo q_lo| ≤ 2^-16 |e||q| joins the window's
+// bound (launch_rank_mfma_x's caller, fast_u).  Measured and rejected, the
+// numbers in DESIGN §5 and profiles/r04/rank/: a separate correction
+// accumulator, a 4-stage ring at two workgroups per CU, 64 × 32 per wave, a
+// 256-candidate 8-wave tile with 4-6 ring stages, a persistent ring, keeping
+// the lo·lo product.
+// s_waitcnt vmcnt(n) for the DMA counts of the ring (n = younger slabs × CPW)
 __device__ __forceinline__ void wait_vmcnt_dma(int n) {
   switch (n) {
-    case 16: asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); break;
-    case 12: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
-    case 9: asm volatile("s_waitcnt vmcnt(9)" ::: "memory"); break;
-    case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
-    case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
     case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
-    case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
     default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
   }
 }
 
-template <int TQ, int WM = 2>
 struct XTile {
-  static constexpr int BQ = 64 * TQ;                   // queries per workgroup
-  static constexpr int BNX = 64 * WM;                  // candidates per workgroup
-  static constexpr int NT = 128 * WM;                  // threads
-  // bf16 per ring stage: per 128-candidate block E hi | lo (4 KB each), then Q hi | lo (2·TQ KB each)
-  static constexpr int STAGE = (4 * WM + 4 * TQ) * 512;
-  static constexpr int CPW = (4 * WM + 4 * TQ) / (2 * WM);  // 1 KB DMA chunks per wave per slab
-  static_assert((4 * WM + 4 * TQ) % (2 * WM) == 0, "DMA chunks must split evenly over the waves");
+  static constexpr int TQ = 2;                   // 32-query column tiles per wave
+  static constexpr int BQ = 64 * TQ;             // queries per workgroup
+  static constexpr int BNX = 128;                // candidates per workgroup
+  static constexpr int NST = 3;                  // LDS ring stages (NST − 1 slabs in flight)
+  // bf16 per ring stage: E hi | lo (4 KB each), then Q hi | lo (2·TQ KB each)
+  static constexpr int STAGE = (8 + 4 * TQ) * 512;
+  static constexpr int CPW = (8 + 4 * TQ) / 4;   // 1 KB DMA chunks per wave per slab
 };
 
-// NST: LDS ring stages (NST − 1 slabs in flight).  4 by default; the
-// 256-candidate tile can hold 6 (144 KB of ring at one workgroup per CU:
-// KGE_XTILE_WM=4 KGE_XTILE_NST=6).
-// MRG (default; KGE_XTILE_MERGE=0 off): the correction products join each slab's hi·hi
-// chain (one accumulator per 32×32 block instead of two: ≈170 VGPRs, three
-// workgroups per CU on a 3-stage ring); the window's bound grows by the
-// chain's rounding (launch_rank_mfma_x's caller, fast_u).
-template <bool GATHER, int TQ, int WM = 2, bool LL = true, int NST = XS_NST, bool MRG = false>
-__global__ __launch_bounds__(128 * WM, WM == 4 ? 1 : (MRG ? 3 : (TQ == 1 ? 3 : 2))) void k_rank_mfma_x(XArgs a) {
-  using X = XTile<TQ, WM>;
-  static_assert(!GATHER || WM == 2, "the gather pass uses 128-row candidate tiles");
-  static_assert(NST >= 3 && NST <= 6, "ring depth");
+template <bool GATHER>
+__global__ __launch_bounds__(256, 3) void k_rank_mfma_x(XArgs a) {
+  using X = XTile;
+  constexpr int TQ = X::TQ, NST = X::NST;
   // one LDS array: [NST stages][E_hi | E_lo | Q_hi | Q_lo] then arow/brow, sts, sdl, cgt
   __shared__ __attribute__((aligned(16))) uint16_t smem[NST * X::STAGE + 128 * 4 * 2 + 128 * 2 * 2 + 128 * 2 * 3];
   int64_t* arow = reinterpret_cast<int64_t*>(smem + NST * X::STAGE);
@@ -513,28 +498,27 @@ __global__ __launch_bounds__(128 * WM, WM == 4 ? 1 : (MRG ? 3 : (TQ == 1 ? 3 : 2
   const auto rq = buf_rsrc(a.qs, a.qs_bytes);
   const auto re = buf_rsrc(a.es, a.es_bytes);
   const int nslab = a.nslab;
-  // 1 KB chunk c of a stage (LDS bytes c·1024 …): c < 4·WM candidate pieces
-  // (per 128-row block: hi 0-3, lo 4-7; 32 rows each), then the query pieces
-  // (hi, lo: 2·TQ chunks each).  Wave w moves chunks CPW·w … CPW·w + CPW − 1.
+  // 1 KB chunk c of a stage (LDS bytes c·1024 …): c < 8 candidate pieces (hi
+  // 0-3, lo 4-7; 32 rows each), then the query pieces (hi, lo: 2·TQ chunks
+  // each).  Wave w moves chunks CPW·w … CPW·w + CPW − 1.
   int64_t grow[X::CPW];  // GATHER: this lane's source row of each candidate chunk
 #pragma unroll
   for (int k = 0; k < X::CPW; ++k) {
     const int c = X::CPW * w + k;
-    grow[k] = (GATHER && c < 4 * WM) ? brow[(c & 3) * 32 + (lane >> 1)] : 0;
+    grow[k] = (GATHER && c < 8) ? brow[(c & 3) * 32 + (lane >> 1)] : 0;
   }
   const int64_t qrb = (int64_t)ty * X::BQ / 128;           // the queries' 128-row block in the split layout
   const uint32_t qsub = (uint32_t)((ty * X::BQ) & 127) * 32;  // … and their byte offset inside it
-  // each chunk's source offset at slab 0 and its buffer, computed once: a
-  // slab adds its hi + lo pieces (8 KB) in both split layouts, so the loop
-  // only adds sl · 8 KB (GATHER: XS_OOB stays out of range for absent rows)
+  // each chunk's source offset at slab 0, computed once: a slab adds its hi +
+  // lo pieces (8 KB) in both split layouts, so the loop only adds sl · 8 KB
+  // (GATHER: XS_OOB stays out of range for absent rows)
   constexpr uint32_t SLAB_BYTES = 2u * (2u * XS_PIECE);
   uint32_t off0[X::CPW];
 #pragma unroll
   for (int k = 0; k < X::CPW; ++k) {
     const int c = X::CPW * w + k;
-    const bool cand = c < 4 * WM;
-    if (cand) {
-      const int rb = c >> 3, piece = (c >> 2) & 1, sub = c & 3;
+    if (c < 8) {
+      const int piece = (c >> 2) & 1, sub = c & 3;
       if (GATHER) {
         const int64_t r = grow[k];
         // LDS row (lane >> 1) of the chunk, half (lane & 1) holds k-half
@@ -544,11 +528,10 @@ __global__ __launch_bounds__(128 * WM, WM == 4 ? 1 : (MRG ? 3 : (TQ == 1 ? 3 : 2
                                         src_half * 16)
                            : XS_OOB;
       } else {
-        off0[k] = (uint32_t)((((int64_t)tx * (WM / 2) + rb) * nslab * 2 + piece) * (2 * XS_PIECE) + sub * 1024 +
-                             lane * 16);
+        off0[k] = (uint32_t)((((int64_t)tx * nslab * 2 + piece) * (2 * XS_PIECE) + sub * 1024 + lane * 16));
       }
     } else {
-      const int cc = c - 4 * WM, piece = cc / (2 * TQ), sub = cc % (2 * TQ);
+      const int cc = c - 8, piece = cc / (2 * TQ), sub = cc % (2 * TQ);
       off0[k] = (uint32_t)((qrb * nslab * 2 + piece) * (2 * XS_PIECE) + qsub + sub * 1024 + lane * 16);
     }
   }
@@ -558,27 +541,27 @@ __global__ __launch_bounds__(128 * WM, WM == 4 ? 1 : (MRG ? 3 : (TQ == 1 ? 3 : 2
     for (int k = 0; k < X::CPW; ++k) {
       const int c = X::CPW * w + k;
       const uint32_t off = (GATHER && off0[k] == XS_OOB) ? XS_OOB : off0[k] + (uint32_t)sl * SLAB_BYTES;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(c < 4 * WM ? re : rq,
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(c < 8 ? re : rq,
                                                (__attribute__((address_space(3))) void*)(base + c * 512), 16, off, 0,
                                                0, 0);
     }
   };
   // DMAs issued after slab sl's, when sl is waited for: those of the next
   // min(NST − 2, nslab − 1 − sl) slabs, CPW instructions each (vmcnt counts in order)
-  static_assert(X::CPW == 3 || X::CPW == 4, "vmcnt immediates below");
+  static_assert(X::CPW == 4 && NST == 3, "vmcnt immediates of wait_vmcnt_dma");
   auto wait_slab = [&](int sl) {
     const int left = nslab - 1 - sl;
     const int after = left < NST - 2 ? left : NST - 2;
     wait_vmcnt_dma(after * X::CPW);
   };
 
-  f32x16 run[2][TQ], cor[2][TQ], mprev[2][TQ];
+  f32x16 run[2][TQ], mprev[2][TQ];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < TQ; ++j)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) run[i][j][r] = cor[i][j][r] = mprev[i][j][r] = 0.f;
+      for (int r = 0; r < 16; ++r) run[i][j][r] = mprev[i][j][r] = 0.f;
   const f32x16 zero = {};
 
   const int kh = lane >> 5, li = lane & 31;
@@ -610,15 +593,14 @@ __global__ __launch_bounds__(128 * WM, WM == 4 ? 1 : (MRG ? 3 : (TQ == 1 ? 3 : 2
     if (sl + NST - 1 < nslab) issue(sl + NST - 1, (sl + NST - 1) % NST);
     if (!live) continue;
     const uint16_t* Es = smem + (sl % NST) * X::STAGE;
-    const uint16_t* Qh = Es + WM * XS_PIECE;
+    const uint16_t* Qh = Es + 2 * XS_PIECE;
     const uint16_t* Ql = Qh + TQ * 1024;
     bf16x8 eh[2], el[2], qh[TQ], ql[TQ];
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int row = wm * 64 + i * 32 + li;
-      const uint16_t* Eh = Es + (row >> 7) * 2 * XS_PIECE;  // this row's 128-row block: hi, then lo
-      eh[i] = *reinterpret_cast<const bf16x8*>(Eh + (row & 127) * XS_BK + khs * 8);
-      el[i] = *reinterpret_cast<const bf16x8*>(Eh + XS_PIECE + (row & 127) * XS_BK + khs * 8);
+      eh[i] = *reinterpret_cast<const bf16x8*>(Es + row * XS_BK + khs * 8);
+      el[i] = *reinterpret_cast<const bf16x8*>(Es + XS_PIECE + row * XS_BK + khs * 8);
     }
 #pragma unroll
     for (int j = 0; j < TQ; ++j) {
@@ -626,34 +608,24 @@ __global__ __launch_bounds__(128 * WM, WM == 4 ? 1 : (MRG ? 3 : (TQ == 1 ? 3 : 2
       qh[j] = *reinterpret_cast<const bf16x8*>(Qh + row * XS_BK + khs * 8);
       ql[j] = *reinterpret_cast<const bf16x8*>(Ql + row * XS_BK + khs * 8);
     }
-    // the running sum takes the PREVIOUS slab's hi·hi products (long done:
-    // an add right behind the MFMA it reads stalls the wave ~40 cycles), then
-    // this slab's hi·hi and correction MFMAs
+    // the running sum takes the PREVIOUS slab's chain (long done: an add
+    // right behind the MFMA it reads stalls the wave ~40 cycles), then this
+    // slab's hi·hi, hi·lo and lo·hi MFMAs chain from zero
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
       for (int j = 0; j < TQ; ++j) {
         run[i][j] += mprev[i][j];  // (v_pk_add_f32 pairs)
         mprev[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(eh[i], qh[j], zero, 0, 0, 0);
-        if constexpr (MRG) {
-          mprev[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(eh[i], ql[j], mprev[i][j], 0, 0, 0);
-          mprev[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(el[i], qh[j], mprev[i][j], 0, 0, 0);
-          if constexpr (LL) mprev[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(el[i], ql[j], mprev[i][j], 0, 0, 0);
-        } else {
-          cor[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(eh[i], ql[j], cor[i][j], 0, 0, 0);
-          cor[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(el[i], qh[j], cor[i][j], 0, 0, 0);
-          if constexpr (LL) cor[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(el[i], ql[j], cor[i][j], 0, 0, 0);
-        }
+        mprev[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(eh[i], ql[j], mprev[i][j], 0, 0, 0);
+        mprev[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(el[i], qh[j], mprev[i][j], 0, 0, 0);
       }
   }
   f32x16 acc[2][TQ];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int j = 0; j < TQ; ++j) {
-      if constexpr (MRG) acc[i][j] = run[i][j] + mprev[i][j];
-      else acc[i][j] = (run[i][j] + mprev[i][j]) + cor[i][j];
-    }
+    for (int j = 0; j < TQ; ++j) acc[i][j] = run[i][j] + mprev[i][j];
 
   // C/D layout as the fp32 tile: col (query) = lane & 31, row (candidate) = (reg & 3) + 8·(reg >> 2) + 4·(lane >> 5)
   if (GATHER) {
@@ -679,11 +651,10 @@ __global__ __launch_bounds__(128 * WM, WM == 4 ? 1 : (MRG ? 3 : (TQ == 1 ? 3 : 2
     const uint32_t ex[2] = {exw[j][0], exw[j][1]};
     // branch-free count; the rare near-ties collect in a bit mask and are
     // listed in one loop afterwards (a branch per candidate cost more than
-    // the count itself)
-    // an excluded candidate's score becomes −∞ first: then "counted" is
-    // d > δ and "near" is |d| ≤ δ (−δ ≤ d ≤ δ; false for −∞ and NaN), the
-    // same sets as ok ∧ d > δ and ok ∧ ¬(d > δ) ∧ d ≥ −δ with fewer live
-    // compare masks
+    // the count itself).  An excluded candidate's score becomes −∞ first:
+    // then "counted" is d > δ and "near" is |d| ≤ δ (−δ ≤ d ≤ δ; false for −∞
+    // and NaN), the same sets as ok ∧ d > δ and ok ∧ ¬(d > δ) ∧ d ≥ −δ with
+    // fewer live compare masks
     int g = 0;
     uint32_t near = 0;  // bit 16·i + r
 #pragma unroll
@@ -711,246 +682,6 @@ __global__ __launch_bounds__(128 * WM, WM == 4 ? 1 : (MRG ? 3 : (TQ == 1 ? 3 : 2
   }
   __syncthreads();
   if (t < X::BQ && arow[t] >= 0 && cgt[t]) atomicAdd(&a.gt[q0 + t], cgt[t]);
-}
-
-// Persistent counting pass (KGE_XTILE_PERSIST=1): two 256-thread workgroups
-// per CU for the whole launch, workgroup b running its XCD's tiles
-// i = b/8, b/8 + G/8, … in xcd_tile's group order.  The LDS ring runs on
-// across tiles: the first three slabs of tile t+1 are issued during tile t's
-// last three slabs, so they land during tile t's epilogue and no tile starts
-// on an empty ring.  Everything a tile's epilogue reads besides the scores —
-// s_true and the window per query, each lane's two exclusion-bitmap words —
-// arrives the same way, by LDS-DMA issued with the tile's first slab into one
-// of two metadata buffers, so the explicit vmcnt waits cover it (a plain
-// global load would make the compiler wait for every DMA issued after it).
-// Same slab arithmetic and epilogue as k_rank_mfma_x<false, 2>; needs
-// nslab ≥ 3 (a tile's metadata is issued once the previous tile's is read).
-struct XMeta {  // one metadata buffer (LDS)
-  float st[128], dl[128];
-  uint32_t ex[4][2][2][64];  // [wave][query tile j][candidate word i][lane]
-};
-
-__device__ __forceinline__ void xcd_tile_at(const XArgs& a, int k, int i, int& x, int& y) {
-  const int nxk = (a.gx - k + 7) >> 3;
-  const int per = a.group * a.gy;
-  const int g = i / per, rem = i - g * per;
-  const int gsz = min(a.group, nxk - g * a.group);
-  x = (g * a.group + rem % gsz) * 8 + k;
-  y = rem / gsz;
-}
-
-__device__ __forceinline__ __attribute__((address_space(3))) void* xp_lds(const void* p) {
-  return (__attribute__((address_space(3))) void*)p;
-}
-
-constexpr int XP_MAXT = 256;  // tiles per persistent workgroup (the launcher falls back above)
-
-template <bool LL>
-__global__ __launch_bounds__(256, 2) void k_rank_mfma_xp(XArgs a) {
-  constexpr int TQ = 2;
-  using X = XTile<TQ>;
-  __shared__ __attribute__((aligned(16))) uint16_t smem[XS_NST * X::STAGE];
-  __shared__ __attribute__((aligned(16))) XMeta meta[2];
-  __shared__ int32_t cgt[128];
-  __shared__ int32_t tcoord[XP_MAXT];  // this workgroup's tiles: tx << 16 | ty
-  const int t = threadIdx.x, lane = t & 63, w = wave_id();
-  const int wm = w >> 1, wn = w & 1;
-  const int kx = blockIdx.x & 7, i0 = blockIdx.x >> 3, istride = gridDim.x >> 3;
-  const int nxk = (a.gx - kx + 7) >> 3, ntile = nxk * a.gy;
-  const int my_tiles = (i0 < ntile) ? (ntile - i0 + istride - 1) / istride : 0;
-  if (my_tiles == 0) return;  // (block-uniform)
-  const int nslab = a.nslab;
-  const int total = my_tiles * nslab;
-  for (int k = t; k < my_tiles; k += 256) {
-    int tx, ty;
-    xcd_tile_at(a, kx, i0 + k * istride, tx, ty);
-    tcoord[k] = (tx << 16) | ty;
-  }
-  if (t < 128) cgt[t] = 0;
-  __syncthreads();
-  auto tile = [&](int it, int& tx, int& ty) {
-    const int v = __builtin_amdgcn_readfirstlane(tcoord[it]);
-    tx = v >> 16;
-    ty = v & 0xFFFF;
-  };
-  const auto rq = buf_rsrc(a.qs, a.qs_bytes);
-  const auto re = buf_rsrc(a.es, a.es_bytes);
-  const auto rst = buf_rsrc(a.s_true, (uint64_t)a.nq * 4u);
-  const auto rdl = buf_rsrc(a.win.delta, (uint64_t)a.nq * 4u);
-  const auto rbits = buf_rsrc(a.fbits, (uint64_t)a.nq * (uint64_t)a.W * 4u);
-  const int kh = lane >> 5, li = lane & 31;
-  const int khs = kh ^ ((li >> 3) & 1);  // the k-half's slot in the swapped row
-  const int wq0 = wn * 32 * TQ;
-  // the metadata of tile `it` into buffer it & 1 (issued before that tile's first slab)
-  auto issue_meta = [&](int it, int tx, int ty) {
-    XMeta& mb = meta[it & 1];
-    const int q0 = ty * X::BQ, e0 = tx * X::BNX;
-    if (w < 2) {
-      const int q = q0 + 64 * w + lane;
-      const uint32_t off = (q < a.nq) ? (uint32_t)q * 4u : XS_OOB;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rst, xp_lds(&mb.st[64 * w]), 4, off, 0, 0, 0);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rdl, xp_lds(&mb.dl[64 * w]), 4, off, 0, 0, 0);
-    }
-#pragma unroll
-    for (int j = 0; j < TQ; ++j)
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int q = q0 + wq0 + j * 32 + li;
-        const int widx = (e0 >> 5) + wm * 2 + i;
-        const uint32_t off = (q < a.nq && widx < a.W) ? (uint32_t)((uint64_t)q * (uint64_t)a.W + widx) * 4u : XS_OOB;
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rbits, xp_lds(&mb.ex[w][j][i][0]), 4, off, 0, 0, 0);
-      }
-  };
-  // operand slabs in order g = 0, 1, …: (tile ni_it, slab ni_sl) into ring stage g % XS_NST
-  int ni_it = 0, ni_sl = 0, ng = 0;
-  auto issue_next = [&]() {
-    int tx, ty;
-    tile(ni_it, tx, ty);
-    if (ni_sl == 0) issue_meta(ni_it, tx, ty);
-    const int qrb = ty * X::BQ / 128;
-    const uint32_t qsub = (uint32_t)((ty * X::BQ) & 127) * 32;
-    uint16_t* base = smem + (ng % XS_NST) * X::STAGE;
-#pragma unroll
-    for (int k = 0; k < X::CPW; ++k) {
-      const int c = X::CPW * w + k;
-      uint32_t off;
-      const bool cand = c < 8;
-      if (cand) {
-        const int piece = (c >> 2) & 1, sub = c & 3;
-        off = (uint32_t)(((tx * nslab + ni_sl) * 2 + piece) * (2 * XS_PIECE) + sub * 1024 + lane * 16);
-      } else {
-        const int cc = c - 8, piece = cc / (2 * TQ), sub = cc % (2 * TQ);
-        off = (uint32_t)(((qrb * nslab + ni_sl) * 2 + piece) * (2 * XS_PIECE) + qsub + sub * 1024 + lane * 16);
-      }
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(cand ? re : rq, xp_lds(base + c * 512), 16, off, 0, 0, 0);
-    }
-    ++ng;
-    if (++ni_sl == nslab) {
-      ni_sl = 0;
-      ++ni_it;
-    }
-  };
-  // slab g has landed (and, with it, the metadata issued before it) once at
-  // most the operand DMAs of the (≤ 2) younger slabs are outstanding
-  auto wait_g = [&](int g) {
-    const int after = total - 1 - g;
-    if (after >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    else if (after == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  };
-  const f32x16 zero = {};
-#pragma unroll
-  for (int p = 0; p < XS_NST - 1; ++p)
-    if (p < total) issue_next();
-  int g = 0;
-  for (int it = 0; it < my_tiles; ++it) {
-    int tx, ty;
-    tile(it, tx, ty);
-    const int64_t q0 = (int64_t)ty * X::BQ, e0 = (int64_t)tx * X::BNX;
-    const bool live = q0 + wq0 < a.nq && e0 + wm * 64 < a.E;
-    f32x16 run[2][TQ], cor[2][TQ], mprev[2][TQ];
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < TQ; ++j)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) run[i][j][r] = cor[i][j][r] = mprev[i][j][r] = 0.f;
-    for (int sl = 0; sl < nslab; ++sl, ++g) {
-      wait_g(g);
-      __builtin_amdgcn_s_barrier();  // every wave's DMA of slab g has landed; slab g-1's reads are done
-      if (ng < total) issue_next();  // slab g + XS_NST - 1
-      if (!live) continue;
-      const uint16_t* Eh = smem + (int)(g % XS_NST) * X::STAGE;
-      const uint16_t* El = Eh + XS_PIECE;
-      const uint16_t* Qh = Eh + 2 * XS_PIECE;
-      const uint16_t* Ql = Qh + TQ * 1024;
-      bf16x8 eh[2], el[2], qh[TQ], ql[TQ];
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int row = wm * 64 + i * 32 + li;
-        eh[i] = *reinterpret_cast<const bf16x8*>(Eh + row * XS_BK + khs * 8);
-        el[i] = *reinterpret_cast<const bf16x8*>(El + row * XS_BK + khs * 8);
-      }
-#pragma unroll
-      for (int j = 0; j < TQ; ++j) {
-        const int row = wq0 + j * 32 + li;
-        qh[j] = *reinterpret_cast<const bf16x8*>(Qh + row * XS_BK + khs * 8);
-        ql[j] = *reinterpret_cast<const bf16x8*>(Ql + row * XS_BK + khs * 8);
-      }
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < TQ; ++j) {
-#pragma unroll
-          for (int r = 0; r < 16; r += 2) {
-            f32x2 x = {run[i][j][r], run[i][j][r + 1]};
-            const f32x2 y = {mprev[i][j][r], mprev[i][j][r + 1]};
-            x += y;
-            run[i][j][r] = x.x;
-            run[i][j][r + 1] = x.y;
-          }
-          mprev[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(eh[i], qh[j], zero, 0, 0, 0);
-          cor[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(eh[i], ql[j], cor[i][j], 0, 0, 0);
-          cor[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(el[i], qh[j], cor[i][j], 0, 0, 0);
-          if constexpr (LL) cor[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(el[i], ql[j], cor[i][j], 0, 0, 0);
-        }
-    }
-    // epilogue: the metadata of this tile landed with its first slab
-    const XMeta& mb = meta[it & 1];
-    if (live) {
-#pragma unroll
-      for (int j = 0; j < TQ; ++j) {
-        const int n = wq0 + j * 32 + li;
-        const int64_t q = q0 + n;
-        const float st = mb.st[n], dlt = mb.dl[n];
-        const int64_t widx0 = (e0 >> 5) + wm * 2;
-        uint32_t ex[2];
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-          uint32_t word = (q < a.nq && widx0 + i < a.W) ? mb.ex[w][j][i][lane] : ~0u;
-          const int64_t valid = a.E - (e0 + wm * 64 + i * 32);
-          if (valid < 32) word |= (valid <= 0) ? ~0u : (~0u << valid);
-          ex[i] = word;
-        }
-        f32x16 acc[2];
-#pragma unroll
-        for (int i = 0; i < 2; ++i) acc[i] = (run[i][j] + mprev[i][j]) + cor[i][j];
-        int gcount = 0;
-        uint32_t near = 0;
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int mloc = (r & 3) + 8 * (r >> 2) + 4 * kh;
-            const bool ok = ((ex[i] >> mloc) & 1u) == 0u;
-            const float diff = acc[i][r] - st;
-            gcount += (ok && diff > dlt) ? 1 : 0;
-            near |= (ok && !(diff > dlt) && diff >= -dlt) ? (1u << (16 * i + r)) : 0u;
-          }
-        if (__builtin_amdgcn_ballot_w64(near != 0u)) {
-          while (near) {
-            const int b = __builtin_ctz(near);
-            near &= near - 1u;
-            const int i = b >> 4, r = b & 15;
-            const int mloc = (r & 3) + 8 * (r >> 2) + 4 * kh;
-            const int idx = atomicAdd(&a.win.ucnt[q], 1);
-            if (idx < a.win.cap) a.win.ulist[q * (int64_t)a.win.cap + idx] = (int32_t)(e0 + wm * 64 + i * 32 + mloc);
-          }
-        }
-        gcount += __shfl_xor(gcount, 32);
-        if (kh == 0 && q < a.nq && gcount) atomicAdd(&cgt[n], gcount);
-      }
-    }
-    // the tile's counts to global (one atomic per query); the LDS fence-free
-    // barrier keeps the next tile's DMAs in flight
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    if (t < X::BQ) {
-      const int c = cgt[t];
-      if (c && q0 + t < a.nq) atomicAdd(&a.gt[q0 + t], c);
-      cgt[t] = 0;
-    }
-  }
 }
 
 }  // namespace
@@ -1007,20 +738,6 @@ int launch_rank_mfma(int gather, const float* q, const float* ent, int64_t nq, i
 
 // split-bf16 tile: buffer sizes and launchers (path "mfma")
 int64_t xsplit_nslab(int K) { return (K + XS_BK - 1) / XS_BK; }
-bool xsplit_lolo() {  // default: dropped (9 % faster tile, profiles/r04/rank/ab_tile_wm_lolo.txt)
-  const char* e = getenv("KGE_XTILE_LOLO");
-  return e && atoi(e) == 1;
-}
-// default: corrections in the hi·hi chain on the 128-candidate tile (9 %
-// faster, three workgroups per CU; profiles/r04/rank/ab_merged_corrections.txt);
-// KGE_XTILE_MERGE=0: the separate correction accumulator
-bool xsplit_merge() {
-  const char* e = getenv("KGE_XTILE_MERGE");
-  const char* wm = getenv("KGE_XTILE_WM");
-  const char* tq = getenv("KGE_XTILE_TQ");
-  const char* pe = getenv("KGE_XTILE_PERSIST");
-  return !(e && atoi(e) == 0) && !(wm && atoi(wm) == 4) && !(tq && atoi(tq) == 1) && !(pe && atoi(pe) == 1);
-}
 int64_t xsplit_elems(int64_t rows, int K) { return ((rows + 127) / 128) * 128 * xsplit_nslab(K) * XS_BK * 2; }
 
 int launch_split_bf16(const float* src, int64_t rows, int K, uint16_t* dst, hipStream_t s, const int64_t* skip) {
@@ -1040,71 +757,18 @@ int launch_rank_mfma_x(int gather, const uint16_t* qs, const uint16_t* es, int64
   if (qb >= XS_OOB || eb >= XS_OOB) return -1;  // 32-bit buffer offsets, XS_OOB reads zeros
   a.qs_bytes = (uint32_t)qb; a.es_bytes = (uint32_t)eb;
   a.true_id = true_id; a.s_true = s_true; a.fbits = bits; a.W = (E + 31) / 32; a.gt = gt; a.win = win;
-  const char* tq_env = getenv("KGE_XTILE_TQ");  // query tiles per wave (A/B; default 2)
-  const int tq = (tq_env && atoi(tq_env) == 1) ? 1 : 2;
-  const int bq = 64 * tq;
-  const unsigned gy = (unsigned)((nq + bq - 1) / bq);
-  a.gx = (int)((E + BN - 1) / BN);
+  const unsigned gy = (unsigned)((nq + XTile::BQ - 1) / XTile::BQ);
+  a.gx = (int)((E + XTile::BNX - 1) / XTile::BNX);
   a.gy = (int)gy;
   // candidate tiles per L2 group: ≤ 2 MB of split rows (half an XCD's L2)
-  const int64_t tile_bytes = (int64_t)BN * a.nslab * XS_BK * 4;
+  const int64_t tile_bytes = (int64_t)XTile::BNX * a.nslab * XS_BK * 4;
   a.group = (int)std::max<int64_t>(1, (2 << 20) / tile_bytes);
-  if (const char* gg = getenv("KGE_XTILE_GROUP")) a.group = std::max(1, atoi(gg));
-  const bool ll = xsplit_lolo();
   if (gather) {
-    if (tq == 2) {
-      if (ll) hipLaunchKernelGGL((k_rank_mfma_x<true, 2>), dim3(1, gy), dim3(256), 0, s, a);
-      else hipLaunchKernelGGL((k_rank_mfma_x<true, 2, 2, false>), dim3(1, gy), dim3(256), 0, s, a);
-    } else {
-      hipLaunchKernelGGL((k_rank_mfma_x<true, 1>), dim3(1, gy), dim3(256), 0, s, a);
-    }
+    hipLaunchKernelGGL((k_rank_mfma_x<true>), dim3(1, gy), dim3(256), 0, s, a);
     return (int)hipGetLastError();
-  }
-  // KGE_XTILE_PERSIST=1: the persistent form (TQ = 2, WM = 2, ≥ 3 slabs)
-  const char* pe = getenv("KGE_XTILE_PERSIST");
-  int dev = 0, ncu = 256;
-  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) ncu = 256;
-  const unsigned gsz = (unsigned)(((2 * ncu) + 7) / 8 * 8);  // two workgroups per CU, a multiple of the 8 XCDs
-  const int64_t xp_tiles = ((a.gx + 7) / 8 * (int64_t)a.gy + gsz / 8 - 1) / (gsz / 8);  // per workgroup, XCD 0
-  if (tq == 2 && pe && atoi(pe) == 1 && a.nslab >= 3 && xp_tiles <= XP_MAXT && a.gx < 32768 && a.gy < 65536 &&
-      !(getenv("KGE_XTILE_WM") && atoi(getenv("KGE_XTILE_WM")) == 4)) {
-    if (xsplit_lolo()) hipLaunchKernelGGL((k_rank_mfma_xp<true>), dim3(gsz), dim3(256), 0, s, a);
-    else hipLaunchKernelGGL((k_rank_mfma_xp<false>), dim3(gsz), dim3(256), 0, s, a);
-    return (int)hipGetLastError();
-  }
-  // KGE_XTILE_WM=4: 256-candidate tiles, one 8-wave workgroup per CU (TQ = 2)
-  const char* wm_env = getenv("KGE_XTILE_WM");
-  const int wmv = (tq == 2 && wm_env && atoi(wm_env) == 4) ? 4 : 2;
-  if (wmv == 4) {
-    a.gx = (int)((E + 255) / 256);
-    a.group = (int)std::max<int64_t>(1, (2 << 20) / (2 * tile_bytes));
-    if (const char* gg = getenv("KGE_XTILE_GROUP")) a.group = std::max(1, atoi(gg));
   }
   const int64_t per_xcd = (int64_t)((a.gx + 7) / 8) * a.gy;  // XCD 0 has the most candidate tiles
-  const dim3 gs((unsigned)(8 * per_xcd));
-  if (wmv == 4) {
-    // KGE_XTILE_NST=6: a 6-stage ring (5 slabs in flight, 144 KB)
-    const char* nst_env = getenv("KGE_XTILE_NST");
-    const int nst = nst_env ? atoi(nst_env) : 4;
-    if (nst == 6) {
-      if (ll) hipLaunchKernelGGL((k_rank_mfma_x<false, 2, 4, true, 6>), gs, dim3(512), 0, s, a);
-      else hipLaunchKernelGGL((k_rank_mfma_x<false, 2, 4, false, 6>), gs, dim3(512), 0, s, a);
-    } else if (nst == 5) {
-      if (ll) hipLaunchKernelGGL((k_rank_mfma_x<false, 2, 4, true, 5>), gs, dim3(512), 0, s, a);
-      else hipLaunchKernelGGL((k_rank_mfma_x<false, 2, 4, false, 5>), gs, dim3(512), 0, s, a);
-    } else {
-      if (ll) hipLaunchKernelGGL((k_rank_mfma_x<false, 2, 4>), gs, dim3(512), 0, s, a);
-      else hipLaunchKernelGGL((k_rank_mfma_x<false, 2, 4, false>), gs, dim3(512), 0, s, a);
-    }
-  } else if (tq == 2 && xsplit_merge()) {
-    if (ll) hipLaunchKernelGGL((k_rank_mfma_x<false, 2, 2, true, 3, true>), gs, dim3(256), 0, s, a);
-    else hipLaunchKernelGGL((k_rank_mfma_x<false, 2, 2, false, 3, true>), gs, dim3(256), 0, s, a);
-  } else if (!ll && tq == 2)
-    hipLaunchKernelGGL((k_rank_mfma_x<false, 2, 2, false>), gs, dim3(256), 0, s, a);
-  else if (tq == 1)
-    hipLaunchKernelGGL((k_rank_mfma_x<false, 1>), gs, dim3(256), 0, s, a);
-  else
-    hipLaunchKernelGGL((k_rank_mfma_x<false, 2>), gs, dim3(256), 0, s, a);
+  hipLaunchKernelGGL((k_rank_mfma_x<false>), dim3((unsigned)(8 * per_xcd)), dim3(256), 0, s, a);
   return (int)hipGetLastError();
 }
 

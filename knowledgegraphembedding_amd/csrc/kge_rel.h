@@ -16,9 +16,8 @@ namespace kge {
 // not set by this path)
 template <int U, bool P4 = false>
 __device__ __forceinline__ void rel_row_chunks(const RelArgs& a, int64_t rr, int lane) {
-  // a.pos (the single-call step, no CSR): the rows of this relation found by
-  // scanning the batch's relation ids, ascending — the CSR bucket's order
-  const int32_t b0 = a.pos ? 0 : a.off[a.E + rr], b1 = a.pos ? 0 : a.off[a.E + rr + 1];
+  // the rows of this relation: its CSR bucket (ascending occurrence ids)
+  const int32_t b0 = a.off[a.E + rr], b1 = a.off[a.E + rr + 1];
   const float* row = a.rel + rr * a.Lr;
   const bool v4 = (a.Lr % 4) == 0;
   const int nchunk = v4 ? a.Lr / 4 : a.Lr;  // float4 chunks, or single floats
@@ -30,7 +29,7 @@ __device__ __forceinline__ void rel_row_chunks(const RelArgs& a, int64_t rr, int
 #pragma unroll
       for (int e = 0; e < 4; ++e) acc[u][e] = 0.f;
     int32_t p = b0;
-    if (P4 && v4 && !a.pos) {
+    if (P4 && v4) {
       // four occurrences' rows in flight per iteration (a relation can have
       // thousands of occurrences in a large global batch); the sums keep the
       // ascending occurrence order, so the bits are those of the plain loop
@@ -53,40 +52,9 @@ __device__ __forceinline__ void rel_row_chunks(const RelArgs& a, int64_t rr, int
           }
       }
     }
-    // the occurrences in order: the CSR bucket's, or (a.pos) the rows whose
-    // relation is rr, found 64 batch rows at a time
-    // (a.pos: the relation ids of the next four 64-row chunks are loaded
-    // ahead in a register queue, so a wave's scan of a 1024-row batch waits
-    // on ≈4 load latencies, not 16)
-    int64_t r0 = 0;
-    uint64_t mask = 0;
-    auto rel_id = [&](int64_t ii) -> int64_t { return (ii < a.B) ? a.pos[ii * 3 + 1] : -1; };
-    int64_t v0 = -1, v1 = -1, v2 = -1, v3 = -1;
-    if (a.pos) {
-      v0 = rel_id(lane);
-      v1 = rel_id(64 + lane);
-      v2 = rel_id(128 + lane);
-      v3 = rel_id(192 + lane);
-    }
-    while (true) {
-      int64_t i;
-      if (!a.pos) {
-        if (p >= b1) break;
-        i = a.occ[p++] - a.Bn - 2 * a.B;
-      } else {
-        while (!mask && r0 < a.B) {
-          mask = __ballot(v0 == rr);
-          v0 = v1;
-          v1 = v2;
-          v2 = v3;
-          v3 = rel_id(r0 + 256 + lane);
-          r0 += 64;
-        }
-        if (!mask) break;
-        const int b = __builtin_ctzll(mask);
-        mask &= mask - 1;
-        i = r0 - 64 + b;
-      }
+    // the occurrences in order (the rest of the bucket)
+    for (; p < b1; ++p) {
+      const int64_t i = a.occ[p] - a.Bn - 2 * a.B;
       const float* src = a.rel_contrib + i * a.Lr;
 #pragma unroll
       for (int u = 0; u < U; ++u) {

@@ -144,20 +144,63 @@ def shared_seed(group=None) -> int:
     return int(seed[0])
 
 
-def make_train_iterator(args, train_triples, nentity, nrelation, rank=0, world=1, seed=None):
+WORKER_START_METHOD = "forkserver"
+
+
+def worker_context(method=None):
+    """The multiprocessing context of the host DataLoader workers.
+
+    The reference's workers are fork()ed from its training process
+    (run.py:246-260, torch's default).  Here that process holds a HIP
+    context — and, under torchrun, an RCCL communicator — whose runtime
+    threads (ROCr's async-event thread, RCCL's proxy / bootstrap threads,
+    c10d's watchdog and store threads) may hold their locks at the moment of
+    the fork, and whose heap still holds device-side objects — CUDA / pinned
+    tensors, events, communicator work items — in uncollected reference
+    cycles.  A fork copies one thread and all of that memory: when the
+    child's cyclic GC frees one of those objects, torch's caching allocators
+    call into the HIP runtime of a process that no longer has one (its
+    service threads did not survive the fork), or the child blocks on a lock
+    a parent thread held — the worker never answers and the trainer waits on
+    it forever (the round-4 GPU-suite hang: run.py's DataLoader forked from a
+    pytest process after an RCCL group had been created and destroyed in it;
+    DESIGN §12).  Workers therefore start from a "forkserver": a fresh
+    interpreter launched (fork + exec, no GPU state) the first time a context
+    is asked for — run.py asks before it initialises RCCL or the GPU — which
+    forks every worker from its own clean state.  Worker seeding is
+    DataLoader's own (base seed from the loader's generator, numpy seeded
+    from it in the worker), so the batches are the reference's bit for bit
+    (tests/test_run_shard.py compares them with fork-started workers)."""
+    import multiprocessing as mp
+    method = method or WORKER_START_METHOD
+    ctx = mp.get_context(method)
+    if method == "forkserver":
+        from multiprocessing import forkserver
+        if not getattr(worker_context, "_preloaded", False):
+            # the workers' imports, once, in the server (each fork inherits them)
+            ctx.set_forkserver_preload(["torch", "numpy", "knowledgegraphembedding_amd.dataloader"])
+            worker_context._preloaded = True
+        forkserver.ensure_running()
+    return ctx
+
+
+def make_train_iterator(args, train_triples, nentity, nrelation, rank=0, world=1, seed=None, start_method=None):
     """run.py:246-259's two DataLoaders and BidirectionalOneShotIterator.  One
     process: exactly the reference's (shuffle=True on torch's global
     generator).  Under data parallelism each rank gets a disjoint shard of
     every epoch's permutation (RankShardSampler, `seed` — shared_seed() by
     default — the same on all ranks) and its own generator, so its workers'
-    numpy streams — the negatives — differ from the other ranks' too."""
+    numpy streams — the negatives — differ from the other ranks' too.
+    Workers start from worker_context(start_method) (forkserver by default:
+    never a fork of a process that holds GPU / RCCL state)."""
     if world > 1 and seed is None:
         seed = shared_seed(getattr(args, 'dp_group', None))
+    ctx = worker_context(start_method)
 
     def loader(mode):
         ds = TrainDataset(train_triples, nentity, nrelation, args.negative_sample_size, mode)
         kw = dict(batch_size=args.batch_size, num_workers=max(1, args.cpu_num // 2),
-                  collate_fn=TrainDataset.collate_fn)
+                  collate_fn=TrainDataset.collate_fn, multiprocessing_context=ctx)
         if world <= 1:
             return DataLoader(ds, shuffle=True, **kw)
         return DataLoader(ds, sampler=RankShardSampler(len(ds), rank, world, seed + (mode == 'tail-batch')),
@@ -213,6 +256,8 @@ def main(args):
         raise ValueError('one of init_checkpoint/data_path must be choosed.')
     if args.do_train and args.save_path is None:
         raise ValueError('Where do you want to save your trained model?')
+    if args.do_train and not getattr(args, 'device_sampler', False):
+        worker_context()  # the DataLoader workers' server starts before RCCL / HIP exist in this process
     rank = _init_distributed(args)
     if args.save_path and not os.path.exists(args.save_path) and rank == 0:
         os.makedirs(args.save_path)

@@ -518,31 +518,23 @@ def test_config2_full_size_properties():
                                       ("ComplEx", 1000, 24)])
 def test_entity_pass_column_slices_bitwise(name, d, B, monkeypatch):
     """The column-sliced entity pass (k_entity_sl with nsl = 1, 2, 4, 8
-    slices — the count is picked per shape — with the q slices loaded into
-    registers or staged by LDS-DMA) and the row-per-wave pass
-    (k_entity, the path for rows that are not float4-aligned; KGE_ENT_SLICES=0
-    forces it here) apply the same per-element arithmetic in the same
-    occurrence order: identical gradients and fused Adam updates, bit for bit
-    (the regulariser's partial sums only regroup).  d = 1000 (250 slots per
-    (half) row, 4 slices): the line-aligned slices (the default there, rows of
-    16-B phase 0/4 — DistMult 0/2/4/6) against the even split (KGE_ENT_ALIGN=0,
-    suffix "u")."""
+    slices — the count is picked per shape — reading k_row's slice-major q
+    copy in the single-call step) and the row-per-wave pass (k_entity, the
+    path for rows that are not float4-aligned; KGE_ENT_SLICES=0 forces it
+    here) apply the same per-element arithmetic in the same occurrence order:
+    identical gradients and fused Adam updates, bit for bit (the regulariser's
+    partial sums only regroup).  The row-major q / line-aligned slices of the
+    phased and exchanged steps: test_phased_step_bitwise_equals_single_call,
+    test_dp_factors_gpu, test_dp_owner_gpu."""
     E, R, n = 300, 7, 40   # d = 200: 50 slots per (half) row: 1..8 slices all fit
     args = Namespace(negative_adversarial_sampling=True, adversarial_temperature=1.0, uni_weight=False,
                      regularization=1e-4 if name in ("ComplEx", "DistMult") else 0.0)
     pos, neg, w = synth.kge_batch(88, B, n, E, R)
     P, N, W = torch.from_numpy(pos).to(DEV), torch.from_numpy(neg).to(DEV), torch.from_numpy(w).to(DEV)
     out = {}
-    # "<slices>d": the same slices with the q slices staged by LDS-DMA (KGE_ENT_DMA=1)
-    # "q": the slice-major q (with the occurrence buckets); "qc": the same with the CSR
-    variants = {200: ("0", "1", "2", "4", "8", "1d", "4d", "8d", "4q", "4qc"),
-                1000: ("0", "4", "4u", "4d", "4ud", "4q", "4qc")}.get(d, ("0", "-1", "-1d", "-1q", "-1qc"))
+    variants = {200: ("0", "1", "2", "4", "8"), 1000: ("0", "4")}.get(d, ("0", "-1"))
     for nsl in variants:
-        monkeypatch.setenv("KGE_ENT_BUCKETS", "0" if "c" in nsl else "1")
-        monkeypatch.setenv("KGE_ENT_SLICES", nsl.rstrip("udqc"))
-        monkeypatch.setenv("KGE_ENT_DMA", "1" if "d" in nsl else "0")
-        monkeypatch.setenv("KGE_ENT_ALIGN", "0" if "u" in nsl else "1")
-        monkeypatch.setenv("KGE_ENT_QSL", "1" if "q" in nsl else "0")
+        monkeypatch.setenv("KGE_ENT_SLICES", nsl)
         m, *_ = build_model(name, E, R, d, 12.0, 5)
         opt = KGEAdam([p for p in m.parameters() if p.requires_grad], lr=1e-3)
         res = []
@@ -556,48 +548,6 @@ def test_entity_pass_column_slices_bitwise(name, d, B, monkeypatch):
         for (l0, g0, p0), (l1, g1, p1) in zip(out["0"], out[nsl]):
             assert torch.equal(g0, g1) and torch.equal(p0, p1), nsl
             torch.testing.assert_close(l0[:4], l1[:4], rtol=1e-6, atol=0)
-
-
-@pytest.mark.parametrize("variant", ["0", "1", "2", "3", "4", "5"])
-@pytest.mark.parametrize("name", NAMES)
-def test_occurrence_buckets_bitwise(name, variant, monkeypatch):
-    """The single-call step's occurrence buckets (k_row's atomics, the entity
-    pass sorting each bucket in registers, the relation rows found by
-    scanning the batch) against the CSR (KGE_ENT_BUCKETS=0): the same
-    occurrence order, so bit-identical gradients, Adam updates and losses —
-    including entities whose occurrences overflow a bucket (> 64: entity 7 is
-    every row's first three negatives, 192 times; entity 11 twice per row for
-    32 rows) and are found by the scan of the whole batch instead, a
-    negative that is also a positive's head, and relations with many rows.
-    Every variant of the bucket pass (KGE_ENT_VARIANT: moments loaded late,
-    6 or 8 q rows in flight, wave-specialised gather and stream waves) gives
-    the same bits."""
-    E, R, d, B, n = 300, 7, 200, 64, 40
-    args = Namespace(negative_adversarial_sampling=True, adversarial_temperature=1.0, uni_weight=False,
-                     regularization=1e-4 if name in ("ComplEx", "DistMult") else 0.0)
-    pos, neg, w = synth.kge_batch(77, B, n, E, R)
-    neg[:, :3] = 7
-    neg[:32, 5:7] = 11
-    pos[:5, 0] = 7
-    P, N, W = torch.from_numpy(pos).to(DEV), torch.from_numpy(neg).to(DEV), torch.from_numpy(w).to(DEV)
-    out = {}
-    monkeypatch.setenv("KGE_ENT_VARIANT", variant)
-    for bk in ("1", "0"):
-        monkeypatch.setenv("KGE_ENT_BUCKETS", bk)
-        m, *_ = build_model(name, E, R, d, 12.0, 5)
-        opt = KGEAdam([p for p in m.parameters() if p.requires_grad], lr=1e-3)
-        res = []
-        for mode in ("tail-batch", "head-batch"):
-            losses = m.compute_train_grads(P, N, W, mode, args, optimizer=opt)
-            opt.step()
-            res.append((losses.cpu().clone(), m.entity_embedding.grad.cpu().clone(),
-                        m.entity_embedding.detach().cpu().clone(), m.relation_embedding.grad.cpu().clone(),
-                        m.relation_embedding.detach().cpu().clone()))
-        out[bk] = res
-    for a, b in zip(out["1"], out["0"]):
-        assert torch.equal(a[0][:4], b[0][:4]), (a[0], b[0])
-        for x, y, what in zip(a[1:], b[1:], ("entity grad", "entity", "relation grad", "relation")):
-            assert torch.equal(x, y), what
 
 
 @pytest.mark.parametrize("name,E,d,B,n", [(nm, 400, 120, 24, 40) for nm in NAMES] +

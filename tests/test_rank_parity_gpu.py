@@ -52,8 +52,7 @@ pytestmark = pytest.mark.gpu
 DEV = torch.device("cuda", 0)
 U = 2.0 ** -24
 EXACT = ("TransE", "DistMult", "ComplEx", "RotatE", "pRotatE")
-PATHS = {"DistMult": ("auto", "auto/lolo", "auto/persist", "auto/wm4n6", "auto/gatherst", "auto/merge", "mfma32", "tile", "scan"),
-         "ComplEx": ("auto", "auto/lolo", "auto/persist", "auto/wm4n6", "auto/gatherst", "auto/merge", "mfma32", "tile", "scan"),
+PATHS = {"DistMult": ("auto", "mfma32", "tile", "scan"), "ComplEx": ("auto", "mfma32", "tile", "scan"),
          "TransE": ("auto", "scan"), "RotatE": ("auto", "scan"), "pRotatE": ("auto", "auto/noscreen", "scan")}
 
 
@@ -128,23 +127,11 @@ def run_case(tag, name, E, R, d, gamma, seed, queries, filters, refs, report):
         base = None
         for path in PATHS[name]:
             import os
-            # "/lolo": the split tile with its lo·lo products; "/noscreen": pRotatE's
-            # listed candidates all go to the host sin (no correctly-rounded screen)
-            os.environ["KGE_XTILE_LOLO"] = "1" if path.endswith("/lolo") else "0"
-            os.environ["KGE_XTILE_PERSIST"] = "1" if path.endswith("/persist") else "0"
-            os.environ["KGE_XTILE_WM"] = "4" if path.endswith("/wm4n6") else "2"
-            os.environ["KGE_XTILE_NST"] = "6" if path.endswith("/wm4n6") else "4"
-            os.environ["KGE_RANK_TRUE_REF"] = "0" if path.endswith("/gatherst") else "1"
-            os.environ["KGE_XTILE_MERGE"] = "1" if path.endswith("/merge") else "0"
+            # "/noscreen": pRotatE's listed candidates all go to the host sin
+            # (the diagnostic switch KGE_RANK_SIN_SCREEN=0: no device screen)
             os.environ["KGE_RANK_SIN_SCREEN"] = "0" if path.endswith("/noscreen") else "1"
             ranks, ties, listed = m.rank_queries(qs, filters, mode, path=path.split("/")[0], listed=True,
                                                  relation_trig=trig)
-            os.environ.pop("KGE_XTILE_LOLO", None)
-            os.environ.pop("KGE_XTILE_PERSIST", None)
-            os.environ.pop("KGE_XTILE_WM", None)
-            os.environ.pop("KGE_XTILE_NST", None)
-            os.environ.pop("KGE_RANK_TRUE_REF", None)
-            os.environ.pop("KGE_XTILE_MERGE", None)
             os.environ.pop("KGE_RANK_SIN_SCREEN", None)
             if base is None:
                 base = (ranks, ties)
@@ -285,37 +272,20 @@ def test_host_sin_matches_reference(golden_info, g_full, capsys):
     assert differ == 0.0, "this host's sin differs from the reference's: pRotatE ranks would follow this host's"
 
 
-@pytest.mark.parametrize("wm", ["2", "2/lolo", "4", "2/persist", "4/nst6", "2/gatherst", "2/merge", "2/merge-lolo"])
 @pytest.mark.parametrize("name,E,d", [("DistMult", 300, 50), ("DistMult", 257, 37), ("DistMult", 1000, 130),
-                                      ("ComplEx", 300, 25), ("ComplEx", 513, 33), ("DistMult", 129, 16)])
-def test_split_bf16_tile_matches_other_paths(name, E, d, wm, monkeypatch):
+                                      ("ComplEx", 300, 25), ("ComplEx", 513, 33), ("DistMult", 129, 16),
+                                      ("DistMult", 300, 1100), ("ComplEx", 257, 530)])
+def test_split_bf16_tile_matches_other_paths(name, E, d):
     """The split-bf16 MFMA tile ("auto" for DistMult / ComplEx) against the
     fp32 paths on shapes its layout pads: E not a multiple of the 128-row
     block, reduction lengths not a multiple of the 16-k slab (and odd ones,
     whose rows are not float4-aligned), plus exact ties — a block of entity
     rows copied from a true entity.  Ranks and tie counts must be identical
     to the wave scan's (reference order after refinement on every path).
-    wm = 4: the 256-candidate tile (KGE_XTILE_WM=4, one 8-wave workgroup per
-    CU), whose candidate tiles span two 128-row blocks of the split layout
-    (E = 129, 257, 300, 513: a last tile with one block past the table);
-    "lolo": with the lo·lo products (KGE_XTILE_LOLO=1; by default they are
-    dropped and the window widened by their bound); "persist": the persistent
-    counting kernel (KGE_XTILE_PERSIST=1, two workgroups per CU for the whole
-    launch, the LDS ring running on across tiles; d ≤ 32 has < 3 slabs and
-    falls back to the plain kernel); "nst6": the 256-candidate tile with a
-    6-stage LDS ring (KGE_XTILE_WM=4 KGE_XTILE_NST=6); "gatherst": s_true from
-    the gather-mode tile (KGE_RANK_TRUE_REF=0) instead of the reference-order
-    true score; "merge": the corrections inside each slab's hi·hi chain, three
-    workgroups per CU (KGE_XTILE_MERGE=1), with and without the lo·lo
-    products."""
-    monkeypatch.setenv("KGE_XTILE_WM", wm.split("/")[0])
-    monkeypatch.setenv("KGE_XTILE_LOLO", "1" if wm.endswith("lolo") else "0")
-    monkeypatch.setenv("KGE_XTILE_PERSIST", "1" if wm.endswith("persist") else "0")
-    monkeypatch.setenv("KGE_XTILE_NST", "6" if wm.endswith("nst6") else "4")
-    monkeypatch.setenv("KGE_RANK_TRUE_REF", "0" if wm.endswith("gatherst") else "1")
-    monkeypatch.setenv("KGE_XTILE_MERGE", "1" if "merge" in wm else "0")
-    if wm.endswith("merge-lolo"):
-        monkeypatch.setenv("KGE_XTILE_LOLO", "1")
+    Rows of more than 1024 floats (d = 1100, ComplEx 2·530) take the tile's
+    own gather mode for s_true instead of the reference-order true score
+    (whose LDS staging holds ≤ 1024 floats), with the window covering both
+    fast scores."""
     R = 7
     m, ent, rel, _, _ = build(name, E, R, d, 12.0, 17)
     with torch.no_grad():
@@ -338,22 +308,14 @@ def test_split_bf16_tile_matches_other_paths(name, E, d, wm, monkeypatch):
             assert np.array_equal(r, r0) and np.array_equal(t, t0), (name, E, d, mode, p)
 
 
-@pytest.mark.parametrize("wm", ["2", "2/lolo", "4", "2/persist", "4/nst6", "2/gatherst", "2/merge", "2/merge-lolo"])
-@pytest.mark.parametrize("name", ["DistMult", "ComplEx"])
-def test_split_bf16_tile_wide_dynamic_range(name, wm, monkeypatch):
+@pytest.mark.parametrize("name,d", [("DistMult", 48), ("ComplEx", 48), ("DistMult", 1040)])
+def test_split_bf16_tile_wide_dynamic_range(name, d):
     """The split tile's error bound is rigorous, not statistical: entity and
     relation values spread over 10^-30 … 10^3 (bf16 lo pieces and products
     that underflow, rows that differ by 30 orders of magnitude, exact zeros)
-    must still give the wave scan's ranks and ties."""
-    monkeypatch.setenv("KGE_XTILE_WM", wm.split("/")[0])
-    monkeypatch.setenv("KGE_XTILE_LOLO", "1" if wm.endswith("lolo") else "0")
-    monkeypatch.setenv("KGE_XTILE_PERSIST", "1" if wm.endswith("persist") else "0")
-    monkeypatch.setenv("KGE_XTILE_NST", "6" if wm.endswith("nst6") else "4")
-    monkeypatch.setenv("KGE_RANK_TRUE_REF", "0" if wm.endswith("gatherst") else "1")
-    monkeypatch.setenv("KGE_XTILE_MERGE", "1" if "merge" in wm else "0")
-    if wm.endswith("merge-lolo"):
-        monkeypatch.setenv("KGE_XTILE_LOLO", "1")
-    E, R, d = 500, 5, 48
+    must still give the wave scan's ranks and ties (d = 1040: s_true from the
+    tile's gather mode)."""
+    E, R = 500, 5
     m, ent, rel, _, _ = build(name, E, R, d, 12.0, 23)
     g = np.random.default_rng(11)
     with torch.no_grad():

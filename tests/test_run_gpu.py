@@ -82,10 +82,9 @@ def test_run_countries_config1_vs_reference_cli(tmp_path, golden_info):
     from conftest import GOLDEN
     ref = golden_info["countries_run"]
     save = str(tmp_path / "save")
-    # in a fresh interpreter, as the reference's own run was: its host
-    # DataLoader forks a worker, and a fork of the long-lived pytest process
-    # (HIP and earlier tests' host threads alive) hung in the worker now and
-    # then; the seeds are set in the same order as before run.main
+    # in a fresh interpreter, as the reference's own run was (the in-process
+    # case, after an RCCL group: test_run_host_workers_after_rccl_group_in_process);
+    # the seeds are set in the same order as before run.main
     import subprocess
     import sys
     code = (f"import sys, numpy as np, torch; np.random.seed({ref['np_seed']}); torch.manual_seed({ref['torch_seed']}); "
@@ -95,6 +94,13 @@ def test_run_countries_config1_vs_reference_cli(tmp_path, golden_info):
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     r = subprocess.run(cmd, cwd=root, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-3000:]
+    _check_countries_run(save, ref)
+
+
+def _check_countries_run(save, ref):
+    """The run's checkpoint directory and logged metrics against the log the
+    reference's own run.py wrote (tests/golden/make_golden.py gen_countries_run)."""
+    from conftest import GOLDEN
     assert sorted(os.listdir(save)) == ref["files"]
     got = {}
     for line in open(os.path.join(save, "train.log")):
@@ -114,6 +120,42 @@ def test_run_countries_config1_vs_reference_cli(tmp_path, golden_info):
     assert set(ckpt) == set(ref_ckpt)
     assert set(ckpt["model_state_dict"]) == set(ref_ckpt["model_state_dict"])
     assert ckpt["model_state_dict"]["entity_embedding"].shape == (271, 128)
+
+
+def test_run_host_workers_after_rccl_group_in_process(tmp_path, golden_info):
+    """run.py --do_train with host DataLoader workers inside
+    the long-lived test process AFTER an RCCL group has been created, used and
+    destroyed in it — the round-4 hang's setting.  The workers
+    start from run.worker_context()'s forkserver, never as forks of this
+    process; BASELINE config 1 (countries_S1, the reference CLI's flags and
+    seeds, 300 steps = dozens of worker restarts across epochs) must finish and
+    log the reference's metrics, so the start method changed no batch."""
+    import socket
+
+    import torch.distributed as dist
+    from conftest import GOLDEN
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    torch.cuda.set_device(0)
+    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    dev = torch.device("cuda", 0)
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1, device_id=dev)
+    t = torch.arange(7, dtype=torch.float32, device=dev)
+    dist.all_reduce(t, async_op=True).wait()
+    assert dist.get_backend() == "nccl" and torch.equal(t.cpu(), torch.arange(7, dtype=torch.float32))
+    dist.destroy_process_group()
+    ref = golden_info["countries_run"]
+    save = str(tmp_path / "save")
+    np.random.seed(ref["np_seed"])
+    torch.manual_seed(ref["torch_seed"])
+    args = run.parse_args(["--cuda"] + ref["flags"] + ["--data_path", str(GOLDEN / "countries_S1"), "-save", save])
+    assert not args.device_sampler and args.do_train
+    run.main(args)
+    from multiprocessing import forkserver
+    assert run.WORKER_START_METHOD == "forkserver" and forkserver._forkserver._forkserver_pid is not None
+    _check_countries_run(save, ref)
 
 
 def _run_rowpart_worker(rank, world, port, data, save, extra=("--device_sampler", "--row_partition")):

@@ -83,6 +83,29 @@ def test_single_process_keeps_reference_loader():
     assert mode == "tail-batch" and p.shape == (4, 3) and n.shape == (4, 4)
 
 
+def test_forkserver_workers_draw_the_fork_workers_batches():
+    """run.py's workers start from a forkserver (worker_context: never a fork
+    of the GPU / RCCL process), the reference's are fork()ed: with the same
+    torch seed both draw the same positives, negatives and weights over two
+    epochs of each loader (DataLoader seeds each worker from the loader's
+    base seed either way), world 1 and a world-2 rank."""
+    triples = _triples()
+    args = Namespace(negative_sample_size=6, batch_size=8, cpu_num=4)
+    for rank, world in ((0, 1), (1, 2)):
+        got = {}
+        for method in ("fork", "forkserver"):
+            torch.manual_seed(23)
+            np.random.seed(5)
+            it = make_train_iterator(args, triples, E, R, rank=rank, world=world, seed=77 if world > 1 else None,
+                                     start_method=method)
+            assert it.iterator_head is not None
+            got[method] = [next(it) for _ in range(2 * 2 * (len(triples) // world // 8 + 1))]
+        for a, b in zip(got["fork"], got["forkserver"]):
+            assert a[3] == b[3]
+            for x, y in zip(a[:3], b[:3]):
+                assert torch.equal(x, y)
+
+
 def test_fewer_triples_than_ranks_raises():
     """with fewer training triples than ranks every shard is empty
     and training would spin on empty batches; the sampler refuses instead."""

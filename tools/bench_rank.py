@@ -4,8 +4,13 @@ wn18rr shape (E=40943, R=11) d=500, all 3134 test triples × both directions
 (6268 queries) through KGEModel.rank_queries (kge_rank_filtered).
 
 Synthetic graph: 93,003 true triples (wn18rr's train+valid+test count) drawn
-uniformly; tables U(-range, range).  Reports queries/s, the launch time, and
-the MFMA roofline (2·nq·E·K flops ÷ time vs 157.3 TF fp32 dense).
+uniformly; tables U(-range, range).  `--shape fb15k`: the FB15k entity /
+relation counts (E=14951, R=1345) with 592,213 true triples and 4096 test
+triples, the shape best_config.sh:3 evaluates RotatE / TransE on.  Reports
+queries/s and the wall time of the whole pass; for the split-bf16 MFMA path
+the roofline is the bf16 flops the matrix cores issue (three bf16 products
+per fp32 product, tile padding included) over the pass's wall time against
+the 2.5 PF bf16 dense spec — as bench.py's `ranking` block.
 --path tile times the register-tiled VALU kernel instead of the MFMA tile for
 DistMult/ComplEx, --path scan the per-pair wave-reduction scan.
 
@@ -25,8 +30,9 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from knowledgegraphembedding_amd import KGEModel, synth  # noqa: E402
 from knowledgegraphembedding_amd.filters import FilterIndex  # noqa: E402
 
-E, R, NTRUE, NTEST = 40943, 11, 93003, 3134
-FP32_PEAK_TF = 157.3
+SHAPES = {"wn18rr": (40943, 11, 93003, 3134, (901, 902, 903, 904)),
+          "fb15k": (14951, 1345, 592213, 4096, (911, 912, 913, 914))}
+BF16_PEAK_TF = 2500.0
 DIMS = {"DistMult": (False, False), "ComplEx": (True, True), "RotatE": (True, False), "TransE": (False, False),
         "pRotatE": (False, False)}
 
@@ -51,21 +57,24 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--path", default="auto", choices=("auto", "mfma", "mfma32", "tile", "scan"))
     ap.add_argument("--cpu-sample", type=int, default=0, help="queries timed through the CPU oracle (0: skip)")
+    ap.add_argument("--shape", default="wn18rr", choices=sorted(SHAPES))
+    ap.add_argument("--gamma", type=float, default=12.0)
     ap.add_argument("--rank-trig", default="reference", choices=("reference", "device"),
                     help="RotatE / pRotatE: the reference's host trig (exact ranks) or device trig")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
-    h = synth.randint(901, (NTRUE,), E)
-    r = synth.randint(902, (NTRUE,), R)
-    t = synth.randint(903, (NTRUE,), E)
+    E, R, NTRUE, NTEST, seeds = SHAPES[a.shape]
+    h = synth.randint(seeds[0], (NTRUE,), E)
+    r = synth.randint(seeds[1], (NTRUE,), R)
+    t = synth.randint(seeds[2], (NTRUE,), E)
     true = np.unique(np.stack([h, r, t], 1), axis=0)
-    test = true[synth.randint(904, (NTEST,), len(true))]
+    test = true[synth.randint(seeds[3], (NTEST,), len(true))]
     index = FilterIndex(true, E, R)
     out = []
     for name in a.models:
         de, dr = DIMS[name]
         torch.manual_seed(0)
-        m = KGEModel(name, E, R, a.hidden_dim, 12.0, de, dr).to(dev)
+        m = KGEModel(name, E, R, a.hidden_dim, a.gamma, de, dr).to(dev)
         m.rank_trig = a.rank_trig
         K = m.entity_dim
         times = []
@@ -82,16 +91,19 @@ def main():
         dt = min(times)
         nq = 2 * NTEST
         flops = 2.0 * nq * E * K
-        res = {"model": name, "hidden_dim": a.hidden_dim, "entity_dim": K, "queries": nq,
+        res = {"model": name, "shape": a.shape, "entities": E, "hidden_dim": a.hidden_dim, "entity_dim": K, "queries": nq,
                "seconds": dt, "queries_per_s": nq / dt, "candidate_scores_per_s": nq * E / dt,
                "tflops": flops / dt / 1e12,
                "path": rank_path(name, K, a.path), "rank_trig": a.rank_trig,
                "pair_terms_per_s": nq * E * (K // 2 if name in ("RotatE", "ComplEx") else K) / dt,
                "mrr": float(np.mean(1.0 / ranks)),
                "listed_per_query": float(np.mean(np.concatenate([lh, lt])))}
-        if res["path"].startswith("mfma"):
-            res["roofline"] = {"bound": "mfma", "achieved": res["tflops"], "peak": FP32_PEAK_TF, "unit": "TFLOP/s",
-                               "frac": res["tflops"] / FP32_PEAK_TF}
+        if res["path"] == "mfma-split-bf16":
+            pad = lambda x, m: -(-x // m) * m  # noqa: E731
+            issued = 2.0 * 3 * 2 * pad(NTEST, 128) * pad(E, 128) * pad(K, 16)  # three bf16 products per fp32 one
+            res["roofline"] = {"bound": "mfma", "achieved": issued / dt / 1e12, "peak": BF16_PEAK_TF,
+                               "unit": "TFLOP/s", "frac": issued / dt / 1e12 / BF16_PEAK_TF,
+                               "what": "issued bf16 MFMA flops / whole-pass wall time / 2.5 PF bf16 dense spec"}
         if a.cpu_sample:
             from oracle import kge_oracle as O
             ent = m.entity_embedding.detach().cpu()
