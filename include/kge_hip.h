@@ -62,7 +62,7 @@ enum kge_status {
 /* Device-side error bits written to *err_flag. */
 #define KGE_DEVERR_INDEX 1
 #define KGE_DEVERR_SAMPLER 2 /* a row's true list left no room within max_draws draws */
-#define KGE_DEVERR_ARG 4     /* kge_rank_sin_args: item_off does not match the listed counts */
+#define KGE_DEVERR_ARG 4     /* kge_rank_sin_args / finish_sin: item_off or the list stage does not match */
 
 /*
  * The parameters of one KGEModel (model.py:22-70).
@@ -99,9 +99,10 @@ typedef struct kge_model_desc {
 } kge_model_desc;
 
 /* Library identity: "knowledgegraphembedding_amd <KGE_ABI_VERSION> gfx950".  The
- * version changes with every change of a struct or signature in this header;
+ * version changes with every change of a struct, a signature or a call
+ * protocol in this header (0.3: pRotatE's three-call item counts);
  * loaders refuse a library whose version differs from the header they bind. */
-#define KGE_ABI_VERSION "0.2"
+#define KGE_ABI_VERSION "0.3"
 const char *kge_version(void);
 const char *kge_status_string(int status);
 
@@ -456,23 +457,33 @@ int kge_rank_filtered_ex(const kge_model_desc *m, int32_t mode, const int64_t *q
  * CPU vector library's (ATen → MKL VML here), which no device instruction
  * sequence reproduces — in three calls on one stream and workspace:
  *   1. kge_rank_filtered_ex(..., path | KGE_RANK_STAGE_LIST, listed_out): fast
- *      pass, windows widened by the library's ≤ 1 ulp, near-tie lists.
- *   2. the caller reads listed_out and sets item_off [nq + 1] (device int64,
- *      exclusive scan) to n_items(q) = 1 + listed_out[q], or 1 + nentity when
- *      listed_out[q] > KGE_RANK_LIST_CAP (every candidate is rescanned);
- *      kge_rank_sin_args writes args_out [item_off[nq], entity_dim]: per item
- *      (0 = the true entity, then the listed candidates / entity ids in order)
- *      the K phase sums θh + (θr − θt) (head-batch) or (θh + θr) − θt
- *      (tail-batch) the reference takes the sin of (model.py:236-245; IEEE
- *      divisions and adds, host-independent).  A query whose range does not
- *      match its count is skipped and sets KGE_DEVERR_ARG.
+ *      pass, windows widened by the library's ≤ 1 ulp, near-tie lists; then
+ *      every listed candidate's score as an interval under ANY sin within one
+ *      ulp of the exact value, in the reference's operation order (each later
+ *      operation is monotone), and the candidates whose interval clears the
+ *      true score's are decided on the device.  listed_out[q] = the candidates
+ *      left for the library sin (0: the query is fully ranked; > KGE_RANK_LIST_CAP:
+ *      a degenerate window with more undecided candidates than a list, ranked on
+ *      the device with correctly rounded sin instead).
+ *   2. the caller sets item_off [nq + 1] (device int64, exclusive scan) to
+ *      n_items(q) = 1 + listed_out[q] for 1 ≤ listed_out[q] ≤ KGE_RANK_LIST_CAP,
+ *      else 0; kge_rank_sin_args writes args_out [item_off[nq], entity_dim]: per
+ *      item (0 = the true entity, then the listed candidates) the K phase sums
+ *      θh + (θr − θt) (head-batch) or (θh + θr) − θt (tail-batch) the reference
+ *      takes the sin of (model.py:236-245; IEEE divisions and adds,
+ *      host-independent).
  *   3. the caller evaluates sin_values = sin(args) with the reference's own
  *      library call (torch.sin on the host CPU) and kge_rank_finish_sin
  *      re-scores every item from those values in the reference's order
  *      (abs, ATen sum(dim=2), × modulus, γ −) and writes ranks / ties / listed
  *      as kge_rank_filtered_ex does.
- * The queries, filters and mode of step 1 stay in the workspace; steps 2-3
- * pass the same mode, nq and workspace.
+ * Steps 2-3 may be repeated over disjoint subsets of the queries (a query
+ * outside the subset gets 0 items) to bound the caller's buffers; ranks are
+ * final once every query with items has been delivered once.  A query whose
+ * non-empty item range does not hold exactly 1 + listed_out[q] items, a second
+ * delivery of a query, or a call whose mode / nq / entity table differ from the
+ * list stage's (or after another ranking call used the workspace) sets
+ * KGE_DEVERR_ARG.
  */
 int kge_rank_sin_args(const kge_model_desc *m, int32_t mode, int64_t nq, const int64_t *item_off, float *args_out,
                       void *workspace, size_t workspace_bytes, int32_t *err_flag, void *stream);

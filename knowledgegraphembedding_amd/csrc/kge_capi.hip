@@ -69,7 +69,7 @@ int check_model(const kge_model_desc* m, Geom* g) {
 // the others when the reduction length is a multiple of 4, the wave scan
 // otherwise.  Every path ends in the same reference-order refinement, so all
 // give the same ranks.
-enum RankPath : int { RP_AUTO = 0, RP_MFMA = 1, RP_TILE = 2, RP_SCAN = 3, RP_MFMA32 = 4 };
+enum RankPath : int { RP_AUTO = 0, RP_MFMA = 1, RP_TILE = 2, RP_SCAN = 3, RP_MFMA32 = 4, RP_MFMA16 = 5 };
 int rank_path(const kge_model_desc* m, int requested) {
   const bool bil = (m->model == KGE_DISTMULT || m->model == KGE_COMPLEX);
   const bool cplx = (m->model == KGE_ROTATE || m->model == KGE_COMPLEX);
@@ -81,6 +81,8 @@ int rank_path(const kge_model_desc* m, int requested) {
                        (uint64_t)m->nentity * (uint64_t)m->entity_dim * 4u < 0xFFFFFF00ull;
   const bool tile_ok = (K % 4 == 0) && al;
   if (requested == RP_MFMA) return x_ok ? RP_MFMA : -1;
+  // (experiment) the split tile on 16x16x32 MFMAs: s_true in reference order, rows ≤ 1024 floats
+  if (requested == RP_MFMA16) return (x_ok && ((m->entity_dim + 3) & ~3) <= 1024) ? RP_MFMA16 : -1;
   if (requested == RP_MFMA32) return mfma_ok ? RP_MFMA32 : -1;
   if (requested == RP_TILE) return tile_ok ? RP_TILE : -1;
   if (requested == RP_SCAN) return RP_SCAN;
@@ -928,10 +930,10 @@ int kge_adam_step(float* param, const float* grad, float* exp_avg, float* exp_av
 namespace kge {
 namespace {
 struct RankWs {
-  int64_t* tag;  // [8] what the table buffers below hold (k_rank_tag)
-  float *q, *qref, *s_true, *sref_true, *delta, *stats;
+  int64_t* tag;  // [8] what the table buffers below hold (k_rank_tag), then [3] the pRotatE list tag
+  float *q, *qref, *s_true, *sref_true, *sref_hi, *delta, *stats;
   int64_t* true_id;
-  int32_t *gt, *eq, *gtx, *eqx, *ucnt, *ulist;
+  int32_t *gt, *eq, *gtx, *eqx, *ucnt, *done, *ulist;
   uint32_t* bits;
   uint16_t *qs, *es;  // split-bf16 operands (DistMult / ComplEx)
 };
@@ -940,7 +942,7 @@ RankWs carve_rank(void* ws, const kge_model_desc* m, int64_t nq, size_t* bytes) 
   RankWs w;
   // the entity table's own buffers first, at offsets independent of nq, so a
   // later call on the same workspace can reuse them (KGE_RANK_REUSE_TABLE)
-  w.tag = c.take<int64_t>(8);
+  w.tag = c.take<int64_t>(12);
   w.stats = c.take<float>(2 + 2 * TS_BLOCKS);  // [max ‖e‖, max |x|, per-block partials]
   // split-bf16 operands: only where the split tile can run (rank_path's x_ok)
   const bool xs = rank_path(m, RP_MFMA) == RP_MFMA;
@@ -950,13 +952,15 @@ RankWs carve_rank(void* ws, const kge_model_desc* m, int64_t nq, size_t* bytes) 
   w.qref = c.take<float>(nq * (int64_t)m->entity_dim);
   w.s_true = c.take<float>(nq);
   w.sref_true = c.take<float>(nq);
+  w.sref_hi = c.take<float>(nq);
   w.delta = c.take<float>(nq);
   w.true_id = c.take<int64_t>(nq);
-  w.gt = c.take<int32_t>(5 * nq);  // gt, eq, gtx, eqx, ucnt (zeroed by k_rank_prep)
+  w.gt = c.take<int32_t>(6 * nq);  // gt, eq, gtx, eqx, ucnt, done (zeroed by k_rank_prep)
   w.eq = w.gt ? w.gt + nq : nullptr;
   w.gtx = w.gt ? w.gt + 2 * nq : nullptr;
   w.eqx = w.gt ? w.gt + 3 * nq : nullptr;
   w.ucnt = w.gt ? w.gt + 4 * nq : nullptr;
+  w.done = w.gt ? w.gt + 5 * nq : nullptr;
   w.ulist = c.take<int32_t>(nq * (int64_t)RANK_CAP);
   w.bits = c.take<uint32_t>(nq * ((m->nentity + 31) / 32));
   *bytes = c.off + 256;
@@ -1006,7 +1010,7 @@ int rank_impl(const kge_model_desc* m, int32_t mode, const int64_t* queries, int
   const bool reuse = (path & KGE_RANK_REUSE_TABLE) != 0;
   const bool ftab = (path & KGE_RANK_FILTER_TABLE) != 0;  // filt_off / filt_ids: the whole filter index
   path &= ~(KGE_RANK_REUSE_TABLE | KGE_RANK_STAGE_LIST | KGE_RANK_FILTER_TABLE);
-  if (path < RP_AUTO || path > RP_MFMA32) return KGE_ERR_ARG;
+  if (path < RP_AUTO || path > RP_MFMA16) return KGE_ERR_ARG;
   if (nq == 0) return KGE_OK;
   if (nq > 65535) return KGE_ERR_DIM;  // the bitmap launch puts queries on grid.y
   const int rp = rank_path(m, path);
@@ -1053,15 +1057,27 @@ int rank_impl(const kge_model_desc* m, int32_t mode, const int64_t* queries, int
   ra.trig = trig;
   ra.item_off = item_off; ra.sins = sins; ra.args = args;
   ra.lib_sin = (stage != RS_ALL) ? 1 : 0;
+  ra.sref_hi = w.sref_hi; ra.done = w.done;
+  // the list tag of pRotatE's three-call form: the later stages must name the
+  // list stage's mode, nq and table (a reused or switched
+  // workspace gave wrong ranks with no error)
+  const int64_t ltag_v[3] = {(int64_t)0x4B47454C00000000ll | (int64_t)mode, nq,
+                             (int64_t)(uintptr_t)m->entity_embedding};
+  ra.ltag = w.tag ? w.tag + 8 : nullptr;
+  for (int k = 0; k < 3; ++k) ra.ltag_v[k] = ltag_v[k];
   // the split-bf16 tile's error bound in units of u·‖q‖·max‖e‖ (kge_rank_mfma.hip): splitting
   // residuals and the final add 513.2, the dropped lo·lo products 256·(1 + 2^-8)^2 = 258.1, the
   // slab's three chained MFMAs 97.6, the running sum 1.02·nslab
-  const int64_t xns = xsplit_nslab(m->entity_dim);
-  ra.fast_u = (rp != RP_MFMA) ? 0.f : (float)(513.2 + 258.1 + 97.6 + 1.02 * xns);
+  const int64_t xns = xsplit_nslab(m->entity_dim, 0);
+  ra.fast_u = (rp == RP_MFMA)     ? (float)(513.2 + 258.1 + 97.6 + 1.02 * xns)
+              : (rp == RP_MFMA16) ? (float)(513.2 + 258.1 + 195.1 + 1.02 * (xsplit_nslab(m->entity_dim, 1) / 2))
+                                  : 0.f;
   if (stage == RS_ARGS) return launch_status(ops.rank_ref(mode, 3, ra, s));
   EmitArgs ea;
   ea.gt = w.gt; ea.eq = w.eq; ea.gtx = w.gtx; ea.eqx = w.eqx; ea.ucnt = w.ucnt; ea.true_id = w.true_id;
   ea.nq = nq; ea.cap = RANK_CAP; ea.ranks = ranks_out; ea.ties = ties_out; ea.listed = listed_out;
+  ea.ltag = nullptr;
+  for (int k = 0; k < 3; ++k) ea.ltag_v[k] = ltag_v[k];
 
   if (stage != RS_FINISH) {
     g_rank_timer.mark(s);  // (rank timer) 0: the call starts
@@ -1078,7 +1094,7 @@ int rank_impl(const kge_model_desc* m, int32_t mode, const int64_t* queries, int
     // says this workspace already holds them for this table (k_rank_tag)
     const bool need_stats = (m->model == KGE_DISTMULT || m->model == KGE_COMPLEX || m->model == KGE_PROTATE);
     st = launch_status(launch_rank_tag(w.tag, m->entity_embedding, m->nentity, m->entity_dim, reuse ? 1 : 0,
-                                       need_stats ? 1 : 0, rp == RP_MFMA ? 1 : 0, s));
+                                       need_stats ? 1 : 0, rp == RP_MFMA ? 1 : (rp == RP_MFMA16 ? 2 : 0), s));
     if (st) return st;
     if (need_stats) {
       st = launch_status(launch_table_stats(m->entity_embedding, m->nentity, m->entity_dim, w.stats, s, w.tag + 5));
@@ -1093,11 +1109,12 @@ int rank_impl(const kge_model_desc* m, int32_t mode, const int64_t* queries, int
     // split-bf16 path: s_true in the reference's order after the window
     // (k_rank_true_ref, rows of ≤ 1024 floats: its LDS); wider rows take the
     // tile's own gather mode here (the window then covers two fast scores)
-    const bool true_ref = rp == RP_MFMA && ((m->entity_dim + 3) & ~3) <= 1024;
-    if (rp == RP_MFMA) {
-      st = launch_status(launch_split_bf16(w.q, nq, m->entity_dim, w.qs, s));
+    const bool true_ref = (rp == RP_MFMA && ((m->entity_dim + 3) & ~3) <= 1024) || rp == RP_MFMA16;
+    if (rp == RP_MFMA || rp == RP_MFMA16) {
+      const int l16 = rp == RP_MFMA16 ? 1 : 0;
+      st = launch_status(launch_split_bf16(w.q, nq, m->entity_dim, w.qs, s, nullptr, l16));
       if (!st)
-        st = launch_status(launch_split_bf16(m->entity_embedding, m->nentity, m->entity_dim, w.es, s, w.tag + 6));
+        st = launch_status(launch_split_bf16(m->entity_embedding, m->nentity, m->entity_dim, w.es, s, w.tag + 6, l16));
       if (!st && !true_ref)
         st = launch_status(launch_rank_mfma_x(1, w.qs, w.es, nq, m->nentity, m->entity_dim, w.true_id, w.s_true,
                                               w.bits, w.gt, win, s));
@@ -1117,7 +1134,10 @@ int rank_impl(const kge_model_desc* m, int32_t mode, const int64_t* queries, int
     }
     // 5. fast counting pass: clear cases counted, near-ties listed
     g_rank_timer.mark(s);  // (rank timer) 1: fast pass begins
-    if (rp == RP_MFMA) {
+    if (rp == RP_MFMA16) {
+      st = launch_status(launch_rank_mfma_x16(w.qs, w.es, nq, m->nentity, m->entity_dim, w.true_id, w.s_true,
+                                              w.bits, w.gt, win, s));
+    } else if (rp == RP_MFMA) {
       st = launch_status(launch_rank_mfma_x(0, w.qs, w.es, nq, m->nentity, m->entity_dim, w.true_id, w.s_true,
                                             w.bits, w.gt, win, s));
     } else if (rp == RP_MFMA32) {
@@ -1133,27 +1153,34 @@ int rank_impl(const kge_model_desc* m, int32_t mode, const int64_t* queries, int
     if (st) return st;
     g_rank_timer.mark(s);  // (rank timer) 2: fast pass ends
     if (stage == RS_LIST) {  // the lists stay in the workspace for RS_ARGS / RS_FINISH
-      // pRotatE: the listed candidates re-scored with correctly rounded sin in
-      // the reference's order; those the library sin cannot move past the true
-      // score are counted now, only the rest go to the host (≈ 10× fewer)
+      // pRotatE: every listed candidate's score as an interval under any
+      // library sin within one ulp, in the reference's order; those whose
+      // interval clears the true score's are decided now, only the rest go to
+      // the caller's sin.  Overflowed windows: the same over every candidate
+      // (k_rank_exact_iv).  KGE_RANK_SIN_SCREEN=0 (diagnostic): decide nothing.
       RefArgs rs = ra;
-      rs.screen = env_int("KGE_RANK_SIN_SCREEN", 1) != 0 ? 1 : 0;
+      rs.screen = 1;
+      rs.decide = env_int("KGE_RANK_SIN_SCREEN", 1) != 0 ? 1 : 0;
       rs.ucnt_w = w.ucnt;
       rs.ulist_w = w.ulist;
-      if (rs.screen) {
-        st = launch_status(ops.rank_ref(mode, 1, rs, s));
-        if (st) return st;
-      }
+      st = launch_status(ops.rank_ref(mode, 1, rs, s));
+      if (st) return st;
+      st = launch_status(ops.rank_ref(mode, 5, rs, s));
+      if (st) return st;
       ea.ranks = nullptr;
       ea.ties = nullptr;
+      ea.ltag = w.tag + 8;
       return launch_status(launch_rank_emit(ea, s));
     }
   }
   // 6. refinement in the reference's operation order; exact rescan on overflow
+  // (RS_FINISH: overflowed pRotatE windows were ranked by the list stage)
   st = launch_status(ops.rank_ref(mode, 1, ra, s));
   if (st) return st;
-  st = launch_status(ops.rank_ref(mode, 2, ra, s));
-  if (st) return st;
+  if (stage != RS_FINISH) {
+    st = launch_status(ops.rank_ref(mode, 2, ra, s));
+    if (st) return st;
+  }
   st = launch_status(launch_rank_emit(ea, s));
   if (!st) g_rank_timer.mark(s);  // (rank timer) 3: ranks written
   return st;

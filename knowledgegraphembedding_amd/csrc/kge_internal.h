@@ -198,7 +198,7 @@ struct RankArgs {
   RankWin win;
   int32_t* err;
   int prep_only;        // launch k_rank_prep only (the MFMA / tile paths count on their own)
-  int zero_counts;      // k_rank_prep zeroes gt and the four [nq] counters after it (eq, gtx, eqx, ucnt)
+  int zero_counts;      // k_rank_prep zeroes gt and the five [nq] counters after it (eq, gtx, eqx, ucnt, done)
   const float* trig;    // RotatE: [R, 2, Lr] reference cos | sin of the phases, or null
 };
 
@@ -242,10 +242,17 @@ struct RefArgs {
   const float* sins;       // [item_off[nq], K] or null (refine / exact read it)
   float* args;             // [item_off[nq], K] (k_rank_sin_args writes it)
   int lib_sin;             // window: the reference sin is a library's (≤ 1 ulp), not correctly rounded
-  int screen;              // k_rank_refine (pRotatE, correctly rounded sin): count the listed candidates
-                           // that clear the library-sin bound, keep only the others in the list
+  int screen;              // k_rank_refine (pRotatE list stage): each listed candidate's score interval
+                           // under any library sin within 1 ulp (ref_score_half_prot_bounds); those
+                           // whose interval clears the true one's are decided on the device, only the
+                           // others stay in the list for the library sin
+  int decide;              // (screen) 0: decide nothing, keep every listed candidate (diagnostic)
   int32_t* ucnt_w;         // (screen) the list, rewritten in place
   int32_t* ulist_w;
+  float* sref_hi;          // [nq] (screen) the true score interval's upper end (sref_true: its lower)
+  int32_t* done;           // [nq] finish stage: the query's items were delivered (a second delivery is an error)
+  const int64_t* ltag;     // sin_args / finish: the list tag the list stage wrote, expected = ltag_v
+  int64_t ltag_v[3];
 };
 
 // Register-tiled filtered ranking (kge_kernels.inc, k_rank_tile): 64 queries ×

@@ -104,6 +104,50 @@ __device__ __forceinline__ float half_shfl(float v, int src_hl) {
   return __int_as_float(__builtin_amdgcn_ds_bpermute((base + src_hl) << 2, __float_as_int(v)));
 }
 
+__device__ __forceinline__ tf2 half_shfl(tf2 v, int src_hl) { return tf2{half_shfl(v.x, src_hl), half_shfl(v.y, src_hl)}; }
+
+// ATen's CPU sum(dim=2) over K elements, computed by one 32-lane half-wave
+// (hl = lane within the half; every lane returns the total): 8-float
+// vectors; vector v = 4·row + col over size_ilp = ⌊(K/8)/4⌋ rows
+// (multi_row_sum, cascade levels of 2^lp rows), tail vectors into column 0,
+// columns folded 0+1+2+3, then the scalar tail k ≥ 8·⌊K/8⌋ summed from 0 and
+// the 8 vector lanes added in order.  Lane hl = 8·col + p owns elements
+// 32·row + hl.  T = tf2 runs two sums through the same cascade side by side
+// (the pRotatE screen's lower and upper bounds).
+template <class T, class F>
+__device__ T ref_cascade_half(F elem, int K, int hl) {
+  const int nvec = K / 8;
+  const int size = nvec / 4;
+  const int lp0 = ceil_log2_i(size) / 4;
+  const int lp = lp0 > 4 ? lp0 : 4;
+  const int step = 1 << lp;
+  const int64_t mask = step - 1;
+  T acc[4] = {T{}, T{}, T{}, T{}};
+  int i = 0;
+  while (i + step <= size) {
+    for (int j = 0; j < step; ++j, ++i) acc[0] += elem(32 * i + hl);
+#pragma unroll
+    for (int lv = 1; lv < 4; ++lv) {
+      acc[lv] += acc[lv - 1];
+      acc[lv - 1] = T{};
+      if ((i & (mask << (lv * lp))) != 0) break;
+    }
+  }
+  for (; i < size; ++i) acc[0] += elem(32 * i + hl);
+  T col = acc[0];
+#pragma unroll
+  for (int lv = 1; lv < 4; ++lv) col += acc[lv];
+  if (hl < 8)
+    for (int v = 4 * size; v < nvec; ++v) col += elem(8 * v + hl);
+  const T c1 = half_shfl(col, (hl + 8) & 31), c2 = half_shfl(col, (hl + 16) & 31), c3 = half_shfl(col, (hl + 24) & 31);
+  const T vacc = ((col + c1) + c2) + c3;  // valid in lanes 0..7
+  T fin = T{};
+  for (int k = 8 * nvec; k < K; ++k) fin += elem(k);
+#pragma unroll
+  for (int p = 0; p < 8; ++p) fin += half_shfl(vacc, p);
+  return fin;
+}
+
 // Reference-order score of the candidate row e against the query's reference
 // q, computed by one 32-lane half-wave (hl = lane within the half); every
 // lane of the half returns the score.  q / e: [K] real, or [re K | im K].
@@ -131,43 +175,38 @@ __device__ float ref_score_half(const float* __restrict__ q, const float* __rest
     }
     return ref_finish<M>(acc, c);
   } else {
-    // ATen sum(dim=2): 8-float vectors; vector v = 4·row + col over
-    // size_ilp = ⌊(K/8)/4⌋ rows (multi_row_sum, cascade levels of 2^lp rows),
-    // tail vectors into column 0, columns folded 0+1+2+3, then the scalar
-    // tail k ≥ 8·⌊K/8⌋ summed from 0 and the 8 vector lanes added in order.
-    // Lane hl = 8·col + p owns elements 32·row + hl.
-    const int nvec = K / 8;
-    const int size = nvec / 4;
-    const int lp0 = ceil_log2_i(size) / 4;
-    const int lp = lp0 > 4 ? lp0 : 4;
-    const int step = 1 << lp;
-    const int64_t mask = step - 1;
-    float acc[4] = {0.f, 0.f, 0.f, 0.f};
-    int i = 0;
-    while (i + step <= size) {
-      for (int j = 0; j < step; ++j, ++i) acc[0] += elem(32 * i + hl);
-#pragma unroll
-      for (int lv = 1; lv < 4; ++lv) {
-        acc[lv] += acc[lv - 1];
-        acc[lv - 1] = 0.f;
-        if ((i & (mask << (lv * lp))) != 0) break;
-      }
-    }
-    for (; i < size; ++i) acc[0] += elem(32 * i + hl);
-    float col = acc[0];
-#pragma unroll
-    for (int lv = 1; lv < 4; ++lv) col += acc[lv];
-    if (hl < 8)
-      for (int v = 4 * size; v < nvec; ++v) col += elem(8 * v + hl);
-    const float c1 = half_shfl(col, (hl + 8) & 31), c2 = half_shfl(col, (hl + 16) & 31),
-                c3 = half_shfl(col, (hl + 24) & 31);
-    const float vacc = ((col + c1) + c2) + c3;  // valid in lanes 0..7
-    float fin = 0.f;
-    for (int k = 8 * nvec; k < K; ++k) fin += elem(k);
-#pragma unroll
-    for (int p = 0; p < 8; ++p) fin += half_shfl(vacc, p);
-    return ref_finish<M>(fin, c);
+    return ref_finish<M>(ref_cascade_half<float>(elem, K, hl), c);
   }
+}
+
+// pRotatE: the interval the reference's score must lie in when its sin is a
+// library's whose result is within one ulp of the exact value — one of the
+// two floats around sin(x), so within [prev(r), next(r)] of the correctly
+// rounded r (x is the fp32 phase sum; sin(x) is never a float for x ≠ 0).
+// Every later operation is monotone in its operand — |·| on an interval that
+// does not contain 0, each round-to-nearest add of the sum(dim=2) cascade,
+// the product with the modulus, γ − ·  — so the reference's score lies in
+// [γ − fl(S_hi·mod), γ − fl(S_lo·mod)] (mod ≥ 0; swapped otherwise), S_lo /
+// S_hi the same cascade over the elements' lower / upper |sin| bounds.
+// Returns (lo, hi); NaN in either when an argument is not finite.
+__device__ __forceinline__ tf2 abs_sin_bounds(float x) {
+  const float r = sin_rn(x);
+  const float p = nextafterf(r, -INFINITY), n = nextafterf(r, INFINITY);
+  if (p <= 0.f && n >= 0.f) return tf2{0.f, fmaxf(-p, n)};
+  const float ap = fabsf(p), an = fabsf(n);
+  return (r != r) ? tf2{r, r} : tf2{fminf(ap, an), fmaxf(ap, an)};
+}
+template <int MODE>
+__device__ tf2 ref_score_half_prot_bounds(const float* __restrict__ q, const float* __restrict__ e, int K,
+                                          const Consts& c, int hl) {
+  auto elem = [&](int k) -> tf2 {
+    const float pe = e[k] / c.kappa_p;  // model.py:236 / :238
+    return abs_sin_bounds((MODE == HEAD_BATCH) ? (pe + q[k]) : (q[k] - pe));  // model.py:240-245
+  };
+  const tf2 S = ref_cascade_half<tf2>(elem, K, hl);
+  const float a = S.x * c.modulus, b = S.y * c.modulus;
+  if ((a != a) || (b != b)) return tf2{NAN, NAN};
+  return tf2{c.gamma - fmaxf(a, b), c.gamma - fminf(a, b)};
 }
 
 }  // namespace kge

@@ -25,6 +25,7 @@
 #include <torch/autograd.h>
 #include <torch/library.h>
 
+#include <algorithm>
 #include <array>
 #include <cstring>
 #include <mutex>
@@ -323,31 +324,46 @@ std::tuple<Tensor, Tensor> rank_filtered_cuda(const Tensor& entity, const Tensor
   int32_t* err = error_flag_for(dev).data_ptr<int32_t>();
   void* st = current_stream(dev);
   if (model == KGE_PROTATE) {
-    // bit-exact pRotatE (kge_hip.h, three-call form): the near-ties' phase
-    // sums go through the reference's own sin — ATen's CPU at::sin, the call
-    // model.py:245 makes — and come back for the reference-order re-scoring
+    // bit-exact pRotatE (kge_hip.h, three-call form): the device decides
+    // every near-tie whose score interval under any 1-ulp sin clears the true
+    // score's; the undecided ones' phase sums go through the reference's own
+    // sin — ATen's CPU at::sin, the call model.py:245 makes — and come back for
+    // the reference-order re-scoring, in chunks of ≤ 256 MB of arguments
     Tensor cnt = at::empty({nq}, at::TensorOptions().dtype(at::kInt).device(dev));
     check_status(kge_rank_filtered_ex(&d, (int32_t)mode, q.data_ptr<int64_t>(), nq, off.data_ptr<int64_t>(),
                                       ids.data_ptr<int64_t>(), ranks.data_ptr<int64_t>(), ties.data_ptr<int32_t>(),
                                       cnt.data_ptr<int32_t>(), (int32_t)path | KGE_RANK_STAGE_LIST, ws.data_ptr(),
                                       (size_t)ws.numel(), err, st),
                  "kge_rank_filtered_ex (list)");
-    const Tensor c = cnt.to(at::kCPU);  // sync: the counts size the argument buffer
-    Tensor item_off = at::empty({nq + 1}, at::TensorOptions().dtype(at::kLong));
-    int64_t* io = item_off.data_ptr<int64_t>();
+    const Tensor c = cnt.to(at::kCPU);  // sync: the counts size the argument buffers
     const int32_t* cp = c.data_ptr<int32_t>();
-    io[0] = 0;
-    for (int64_t i = 0; i < nq; ++i) io[i + 1] = io[i] + 1 + (cp[i] > KGE_RANK_LIST_CAP ? d.nentity : cp[i]);
-    const Tensor off_d = item_off.to(dev);
-    Tensor args = at::empty({io[nq], (int64_t)d.entity_dim}, entity.options());
-    check_status(kge_rank_sin_args(&d, (int32_t)mode, nq, off_d.data_ptr<int64_t>(), args.data_ptr<float>(),
-                                   ws.data_ptr(), (size_t)ws.numel(), err, st),
-                 "kge_rank_sin_args");
-    const Tensor sins = at::sin(args.to(at::kCPU)).to(dev);
-    check_status(kge_rank_finish_sin(&d, (int32_t)mode, nq, off_d.data_ptr<int64_t>(), sins.data_ptr<float>(),
-                                     ranks.data_ptr<int64_t>(), ties.data_ptr<int32_t>(), nullptr, ws.data_ptr(),
-                                     (size_t)ws.numel(), err, st),
-                 "kge_rank_finish_sin");
+    const int64_t K = d.entity_dim, budget = (int64_t)256 << 20;
+    auto items_of = [&](int64_t i) -> int64_t {
+      return (cp[i] >= 1 && cp[i] <= KGE_RANK_LIST_CAP) ? 1 + (int64_t)cp[i] : 0;
+    };
+    int64_t lo = 0;
+    do {
+      // the next chunk [lo, hi): consecutive queries with ≤ budget bytes of arguments
+      int64_t hi = lo, bytes = 0;
+      while (hi < nq && (bytes == 0 || bytes + items_of(hi) * K * 4 <= budget)) bytes += items_of(hi++) * K * 4;
+      Tensor item_off = at::zeros({nq + 1}, at::TensorOptions().dtype(at::kLong));
+      int64_t* io = item_off.data_ptr<int64_t>();
+      for (int64_t i = 0; i < nq; ++i) io[i + 1] = io[i] + ((i >= lo && i < hi) ? items_of(i) : 0);
+      const Tensor off_d = item_off.to(dev);
+      Tensor args = at::empty({std::max<int64_t>(io[nq], 1), K}, entity.options());
+      Tensor sins = args;
+      if (io[nq]) {
+        check_status(kge_rank_sin_args(&d, (int32_t)mode, nq, off_d.data_ptr<int64_t>(), args.data_ptr<float>(),
+                                       ws.data_ptr(), (size_t)ws.numel(), err, st),
+                     "kge_rank_sin_args");
+        sins = at::sin(args.to(at::kCPU)).to(dev);
+      }
+      check_status(kge_rank_finish_sin(&d, (int32_t)mode, nq, off_d.data_ptr<int64_t>(), sins.data_ptr<float>(),
+                                       ranks.data_ptr<int64_t>(), ties.data_ptr<int32_t>(), nullptr, ws.data_ptr(),
+                                       (size_t)ws.numel(), err, st),
+                   "kge_rank_finish_sin");
+      lo = hi;
+    } while (lo < nq);
     return {ranks, ties};
   }
   check_status(kge_rank_filtered_ex(&d, (int32_t)mode, q.data_ptr<int64_t>(), nq, off.data_ptr<int64_t>(),

@@ -99,7 +99,8 @@ def raise_device_error_value(dev: torch.device, v: int) -> None:
             raise RuntimeError("negative sampler: a positive's true heads/tails leave too few candidate "
                                "entities (the reference's sampling loop would not terminate)")
         if v & _lib.DEVERR_ARG:
-            raise RuntimeError("kge_rank_sin_args: item offsets do not match the listed near-tie counts")
+            raise RuntimeError("pRotatE three-call ranking: item offsets do not match the listed near-tie counts, or the "
+                               "call does not follow its list stage (mode, nq, table or workspace changed)")
         raise RuntimeError(f"device error flag {v}")
 
 
@@ -394,7 +395,7 @@ def adam_step(param: torch.Tensor, grad: torch.Tensor, exp_avg: torch.Tensor, ex
     )
 
 
-RANK_PATHS = {"auto": 0, "mfma": 1, "tile": 2, "scan": 3, "mfma32": 4}
+RANK_PATHS = {"auto": 0, "mfma": 1, "tile": 2, "scan": 3, "mfma32": 4, "mfma16": 5}
 
 
 def reference_rotation(relation: torch.Tensor, embedding_range: float) -> torch.Tensor:
@@ -491,33 +492,72 @@ def reference_sin(args: torch.Tensor) -> torch.Tensor:
     return torch.sin(args)
 
 
+SIN_CHUNK_BYTES = 256 << 20  # the host sin's argument buffer per round trip (pRotatE three-call form)
+
+
+def _pinned(n: int, dtype, cache: dict, key: str) -> torch.Tensor:
+    """A pinned host buffer of at least n elements, kept for the next call."""
+    buf = cache.get(key)
+    if buf is None or buf.numel() < n:
+        buf = torch.empty(max(n, 1024), dtype=dtype, pin_memory=True)
+        cache[key] = buf
+    return buf[:n]
+
+
 def _rank_protate_library_sin(lib, desc, mode_id, q, nq, off, ids, ranks, ties, lst, flags, ws, st, dev):
     """pRotatE ranks bit-exact to the reference (kge_hip.h: the three-call
-    form): the device lists each query's near-ties, writes the phase sums of
-    the true entity and every listed candidate; the host takes their sin with
-    the reference's own call; the device re-scores them in the reference's
-    order.  One host round trip per call (sync), ≈ items × K × 4 bytes each
-    way (wn18rr, K = 500: ≈ 260 listed per query → ≈ 0.5 MB per query)."""
+    form): the device lists each query's near-ties and decides every one
+    whose score interval — under any sin within one ulp of the exact value —
+    clears the true score's; only the undecided ones (and their query's true
+    entity) go to the host, whose sin is the reference's own call.  Per call:
+    one read-back of the undecided counts, then per chunk of ≤
+    SIN_CHUNK_BYTES of arguments a pinned device → host copy, the host sin and
+    a pinned host → device copy (queries outside the chunk get 0 items)."""
     cnt = torch.empty(nq, dtype=torch.int32, device=dev)
     wsp, wsn, err, s = ws.data_ptr(), ws.numel(), st.err.data_ptr(), _stream(dev)
     _lib.check(lib.kge_rank_filtered_ex(desc, mode_id, q.data_ptr(), nq, off.data_ptr(), ids.data_ptr(),
                                         ranks.data_ptr(), ties.data_ptr(), cnt.data_ptr(),
                                         flags | _lib.RANK_STAGE_LIST, wsp, wsn, err, s),
                "kge_rank_filtered_ex (list)")
-    c = cnt.cpu().numpy().astype(np.int64)  # sync: the item counts size the argument buffer
-    items = np.where(c > _lib.RANK_LIST_CAP, 1 + int(desc.nentity), 1 + c)
-    item_off = np.zeros(nq + 1, dtype=np.int64)
-    np.cumsum(items, out=item_off[1:])
+    cache = st.__dict__.setdefault("_sin_bufs", {})
+    c_host = _pinned(nq, torch.int32, cache, "cnt")
+    c_host.copy_(cnt, non_blocking=True)
+    torch.cuda.current_stream(dev).synchronize()  # the counts size the argument buffers
+    c = c_host.numpy().astype(np.int64)
+    items = np.where((c >= 1) & (c <= _lib.RANK_LIST_CAP), 1 + c, 0)
     K = int(desc.entity_dim)
-    off_d = torch.from_numpy(item_off).to(dev)
-    args = torch.empty((int(item_off[-1]), K), dtype=torch.float32, device=dev)
-    _lib.check(lib.kge_rank_sin_args(desc, mode_id, nq, off_d.data_ptr(), args.data_ptr(), wsp, wsn, err, s),
-               "kge_rank_sin_args")
-    sins = reference_sin(args.cpu()).to(dev)
-    del args
-    _lib.check(lib.kge_rank_finish_sin(desc, mode_id, nq, off_d.data_ptr(), sins.data_ptr(), ranks.data_ptr(),
-                                       ties.data_ptr(), _ptr(lst), wsp, wsn, err, s),
-               "kge_rank_finish_sin")
+    per_q = items * K * 4
+    # chunks of consecutive queries with ≤ SIN_CHUNK_BYTES of arguments each
+    bounds, start, acc = [], 0, 0
+    for qi in np.nonzero(items)[0]:
+        if acc and acc + per_q[qi] > SIN_CHUNK_BYTES:
+            bounds.append((start, int(qi)))
+            start, acc = int(qi), 0
+        acc += int(per_q[qi])
+    bounds.append((start, nq))
+    for lo, hi in bounds:
+        part = np.zeros(nq, dtype=np.int64)
+        part[lo:hi] = items[lo:hi]
+        item_off = np.zeros(nq + 1, dtype=np.int64)
+        np.cumsum(part, out=item_off[1:])
+        total = int(item_off[-1])
+        off_d = torch.from_numpy(item_off).to(dev)
+        args = torch.empty((max(total, 1), K), dtype=torch.float32, device=dev)
+        if total:
+            _lib.check(lib.kge_rank_sin_args(desc, mode_id, nq, off_d.data_ptr(), args.data_ptr(), wsp, wsn, err, s),
+                       "kge_rank_sin_args")
+            a_host = _pinned(total * K, torch.float32, cache, "args").view(total, K)
+            a_host.copy_(args[:total], non_blocking=True)
+            torch.cuda.current_stream(dev).synchronize()
+            s_host = _pinned(total * K, torch.float32, cache, "sins").view(total, K)
+            torch.sin(a_host, out=s_host)  # the reference's own call (reference_sin)
+            args[:total].copy_(s_host, non_blocking=True)  # the sin values, in place of their arguments
+        # (the pinned buffers are reused only after this call's copies: the
+        # next chunk synchronises before it writes them)
+        _lib.check(lib.kge_rank_finish_sin(desc, mode_id, nq, off_d.data_ptr(), args.data_ptr(), ranks.data_ptr(),
+                                           ties.data_ptr(), _ptr(lst), wsp, wsn, err, s),
+                   "kge_rank_finish_sin")
+    torch.cuda.current_stream(dev).synchronize()  # the pinned buffers are free for the next call
 
 
 def sample_negatives(triples: torch.Tensor, batch: torch.Tensor, nentity: int, negative_sample_size: int,

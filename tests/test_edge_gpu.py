@@ -139,3 +139,121 @@ def test_test_step_query_blocks_reuse_the_table(name):
                               torch.from_numpy(w).to(DEV), "tail-batch", args)
         with torch.no_grad():
             m.entity_embedding.add_(m.entity_embedding.grad, alpha=-100.0)
+
+
+@pytest.mark.parametrize("kind", ["identical_rows", "zero_modulus"])
+@pytest.mark.parametrize("mode", ["head-batch", "tail-batch"])
+def test_protate_degenerate_table_library_sin(kind, mode, monkeypatch):
+    """pRotatE with the reference's host sin on a degenerate
+    table — every candidate scores exactly the true score (identical entity
+    rows, or modulus 0), so every query's near-tie window overflows the
+    1024-entry list.  The list stage scans such queries with score intervals
+    (k_rank_exact_iv): more undecided candidates than a list, so they are
+    ranked on the device (correctly rounded sin; identical arguments give
+    identical values under any sin) and NO item goes to the host — the host
+    buffer stays bounded instead of 1 + E items per query.  Ranks: 1, ties:
+    every unfiltered candidate; the same as the device-sin path."""
+    E, R, d = 1500, 3, 16
+    m, *_ = build_model("pRotatE", E, R, d, 6.0, 4)
+    with torch.no_grad():
+        if kind == "identical_rows":
+            m.entity_embedding.copy_(m.entity_embedding[0].expand(E, -1))
+        else:
+            m.modulus.zero_()
+    g = np.random.default_rng(8)
+    q = np.stack([g.integers(0, E, 40), g.integers(0, R, 40), g.integers(0, E, 40)], 1).astype(np.int64)
+    true = np.unique(np.concatenate([q, np.stack([g.integers(0, E, 300), g.integers(0, R, 300),
+                                                  g.integers(0, E, 300)], 1)]), axis=0)
+    calls = []
+    real_sin = torch.sin
+
+    def counting_sin(x, *a, **k):
+        calls.append(int(x.numel()))
+        return real_sin(x, *a, **k)
+
+    monkeypatch.setattr(torch, "sin", counting_sin)
+    m.rank_trig = "reference"
+    ranks, ties, listed = m.rank_queries(q, true, mode, listed=True)
+    monkeypatch.setattr(torch, "sin", real_sin)
+    assert sum(calls) == 0, calls  # nothing left for the host sin
+    assert (listed > 1024).all()
+    m.rank_trig = "device"
+    r_dev, t_dev = m.rank_queries(q, true, mode, path="scan")
+    assert np.array_equal(ranks, r_dev) and np.array_equal(ties, t_dev)
+    assert (ranks == 1).all() and (ties > 0).all()
+
+
+def test_protate_three_call_protocol_checks():
+    """kge_rank_sin_args / kge_rank_finish_sin check that they
+    follow their list stage — the same mode, nq and table, nothing else
+    ranked on the workspace in between — and that a query's items arrive
+    once, with 1 + listed entries; a violation sets KGE_DEVERR_ARG (raised
+    as RuntimeError) instead of returning wrong ranks."""
+    from knowledgegraphembedding_amd import _lib
+    E, R, d = 400, 3, 32
+    m, *_ = build_model("pRotatE", E, R, d, 6.0, 6)
+    with torch.no_grad():  # ten exact copies of entity 5: near-ties only the host sin can order
+        m.entity_embedding[100:110].copy_(m.entity_embedding[5].expand(10, -1))
+    g = np.random.default_rng(2)
+    qs = np.stack([g.integers(0, E, 64), g.integers(0, R, 64), np.full(64, 5)], 1).astype(np.int64)
+    true = np.unique(np.concatenate([qs, np.stack([g.integers(0, E, 900), g.integers(0, R, 900),
+                                                   g.integers(0, E, 900)], 1)]), axis=0)
+    q = torch.from_numpy(qs).to(DEV)
+    from knowledgegraphembedding_amd.filters import FilterIndex
+    off, ids = FilterIndex(true, E, R).filter_csr(qs, "tail-batch")
+    off, ids = torch.from_numpy(off).to(DEV), torch.from_numpy(ids).to(DEV)
+    lib = _lib.load()
+    desc = m.desc()
+    mode = _lib.MODE_IDS["tail-batch"]
+    st = ops.state(DEV)
+    nq = 64
+    ws = st.workspace(lib.kge_rank_workspace_bytes(desc, nq))
+    st.rank_ws_ptr = None
+    ranks = torch.empty(nq, dtype=torch.int64, device=DEV)
+    ties = torch.empty(nq, dtype=torch.int32, device=DEV)
+    cnt = torch.empty(nq, dtype=torch.int32, device=DEV)
+    s = ops._stream(DEV)
+    args_ = (ws.data_ptr(), ws.numel(), st.err.data_ptr(), s)
+
+    def list_stage():
+        _lib.check(lib.kge_rank_filtered_ex(desc, mode, q.data_ptr(), nq, off.data_ptr(), ids.data_ptr(),
+                                            ranks.data_ptr(), ties.data_ptr(), cnt.data_ptr(),
+                                            _lib.RANK_STAGE_LIST, *args_), "list")
+        c = cnt.cpu().numpy().astype(np.int64)
+        items = np.where((c >= 1) & (c <= 1024), 1 + c, 0)
+        io = np.zeros(nq + 1, dtype=np.int64)
+        np.cumsum(items, out=io[1:])
+        return torch.from_numpy(io).to(DEV), int(io[-1])
+
+    # a well-formed round: no error
+    io, total = list_stage()
+    buf = torch.zeros((max(total, 1), d), device=DEV)
+    _lib.check(lib.kge_rank_sin_args(desc, mode, nq, io.data_ptr(), buf.data_ptr(), *args_), "args")
+    buf = torch.sin(buf.cpu()).to(DEV)
+    _lib.check(lib.kge_rank_finish_sin(desc, mode, nq, io.data_ptr(), buf.data_ptr(), ranks.data_ptr(),
+                                       ties.data_ptr(), None, *args_), "finish")
+    ops.raise_on_device_error(DEV)
+    if total:
+        # the same items delivered a second time
+        _lib.check(lib.kge_rank_finish_sin(desc, mode, nq, io.data_ptr(), buf.data_ptr(), ranks.data_ptr(),
+                                           ties.data_ptr(), None, *args_), "finish")
+        with pytest.raises(RuntimeError, match="list stage"):
+            ops.raise_on_device_error(DEV)
+    # another mode than the list stage's
+    io, total = list_stage()
+    buf = torch.zeros((max(total, 1), d), device=DEV)
+    other = _lib.MODE_IDS["head-batch"]
+    _lib.check(lib.kge_rank_sin_args(desc, other, nq, io.data_ptr(), buf.data_ptr(), *args_), "args")
+    if total:
+        with pytest.raises(RuntimeError, match="list stage"):
+            ops.raise_on_device_error(DEV)
+    # another ranking call on the workspace between the list stage and finish
+    io, total = list_stage()
+    _lib.check(lib.kge_rank_filtered_ex(desc, mode, q.data_ptr(), nq, off.data_ptr(), ids.data_ptr(),
+                                        ranks.data_ptr(), ties.data_ptr(), None, 0, *args_), "all")
+    buf = torch.zeros((max(total, 1), d), device=DEV)
+    _lib.check(lib.kge_rank_sin_args(desc, mode, nq, io.data_ptr(), buf.data_ptr(), *args_), "args")
+    if total:
+        with pytest.raises(RuntimeError, match="list stage"):
+            ops.raise_on_device_error(DEV)
+    assert total > 0, "the fixture should leave some near-ties for the host"
