@@ -84,6 +84,88 @@ class TrainDataset(Dataset):
         true_tail = {k: np.array(list(set(v))) for k, v in true_tail.items()}
         return true_head, true_tail
 
+    # The copy a DataLoader worker receives.  run.py starts its workers from a
+    # forkserver (run.worker_context), so every worker unpickles the dataset;
+    # the reference's dicts keyed by tuples take ≈ 8 s to pickle at FB15k's
+    # size (483 k triples), once per worker and epoch.  Workers only call
+    # __getitem__, so they get the triples and this mode's tables as flat
+    # sorted arrays (≈ 15 MB, milliseconds) and look them up by binary search:
+    # the same values (counts, the same true id sets — np.isin's result does
+    # not depend on their order) and the same numpy calls in the same order,
+    # so the same batches (tests/test_run_shard.py).
+    def __getstate__(self):
+        cached = self.__dict__.get('_compact')
+        if cached is not None:  # built once: every later worker start pickles only the arrays
+            return cached
+        t = np.asarray(self.triples, dtype=np.int64).reshape(-1, 3)
+        E, R = int(self.nentity), int(self.nrelation)
+        h, r, tl = t[:, 0], t[:, 1], t[:, 2]
+        # count[(x, y)] = start - 1 + occurrences, y = relation or -relation - 1
+        ck, cn = np.unique(np.concatenate([h * (2 * R) + (r + R), tl * (2 * R) + (R - 1 - r)]), return_counts=True)
+        if self.mode == 'head-batch':
+            key, val = r * E + tl, h        # true_head[(relation, tail)]
+        else:
+            key, val = h * R + r, tl        # true_tail[(head, relation)]
+        kv = np.unique(np.stack([key, val], 1), axis=0)
+        tk, start = np.unique(kv[:, 0], return_index=True)
+        state = {'compact': True, 'len': self.len, 'nentity': E, 'nrelation': R,
+                 'negative_sample_size': self.negative_sample_size, 'mode': self.mode, 'triples': t,
+                 'count_keys': ck, 'count_vals': cn + 3, 'true_keys': tk,
+                 'true_off': np.append(start, len(kv)), 'true_ids': kv[:, 1].copy()}
+        self.__dict__['_compact'] = state
+        return state
+
+    def __setstate__(self, st):
+        E, R = st['nentity'], st['nrelation']
+        self.len, self.nentity, self.nrelation = st['len'], E, R
+        self.negative_sample_size, self.mode = st['negative_sample_size'], st['mode']
+        self.triples = _TripleRows(st['triples'])
+        self.count = _CountTable(st['count_keys'], st['count_vals'], R)
+        table = _TrueTable(st['true_keys'], st['true_off'], st['true_ids'], E if self.mode == 'head-batch' else R)
+        self.true_head, self.true_tail = (table, None) if self.mode == 'head-batch' else (None, table)
+
+
+class _TripleRows:
+    """triples[idx] → (h, r, t) of Python ints, from an [n, 3] array."""
+
+    def __init__(self, arr):
+        self.arr = arr
+
+    def __len__(self):
+        return len(self.arr)
+
+    def __getitem__(self, idx):
+        h, r, t = self.arr[idx].tolist()
+        return h, r, t
+
+
+class _CountTable:
+    """count[(x, y)] of TrainDataset.count_frequency from sorted keys x·2R + (y + R)."""
+
+    def __init__(self, keys, vals, R):
+        self.keys, self.vals, self.R = keys, vals, R
+
+    def __getitem__(self, k):
+        key = k[0] * (2 * self.R) + (k[1] + self.R)
+        i = int(np.searchsorted(self.keys, key))
+        if i == len(self.keys) or self.keys[i] != key:
+            raise KeyError(k)
+        return int(self.vals[i])
+
+
+class _TrueTable:
+    """true_head[(r, t)] / true_tail[(h, r)] from sorted keys a·M + b and a CSR of ids."""
+
+    def __init__(self, keys, off, ids, M):
+        self.keys, self.off, self.ids, self.M = keys, off, ids, M
+
+    def __getitem__(self, k):
+        key = k[0] * self.M + k[1]
+        i = int(np.searchsorted(self.keys, key))
+        if i == len(self.keys) or self.keys[i] != key:
+            raise KeyError(k)
+        return self.ids[self.off[i]:self.off[i + 1]]
+
 
 class TestDataset(Dataset):
     def __init__(self, triples, all_true_triples, nentity, nrelation, mode):
