@@ -69,7 +69,7 @@ int check_model(const kge_model_desc* m, Geom* g) {
 // the others when the reduction length is a multiple of 4, the wave scan
 // otherwise.  Every path ends in the same reference-order refinement, so all
 // give the same ranks.
-enum RankPath : int { RP_AUTO = 0, RP_MFMA = 1, RP_TILE = 2, RP_SCAN = 3, RP_MFMA32 = 4, RP_MFMA16 = 5 };
+enum RankPath : int { RP_AUTO = 0, RP_MFMA = 1, RP_TILE = 2, RP_SCAN = 3, RP_MFMA32 = 4 };
 int rank_path(const kge_model_desc* m, int requested) {
   const bool bil = (m->model == KGE_DISTMULT || m->model == KGE_COMPLEX);
   const bool cplx = (m->model == KGE_ROTATE || m->model == KGE_COMPLEX);
@@ -81,8 +81,6 @@ int rank_path(const kge_model_desc* m, int requested) {
                        (uint64_t)m->nentity * (uint64_t)m->entity_dim * 4u < 0xFFFFFF00ull;
   const bool tile_ok = (K % 4 == 0) && al;
   if (requested == RP_MFMA) return x_ok ? RP_MFMA : -1;
-  // (experiment) the split tile on 16x16x32 MFMAs: s_true in reference order, rows ≤ 1024 floats
-  if (requested == RP_MFMA16) return (x_ok && ((m->entity_dim + 3) & ~3) <= 1024) ? RP_MFMA16 : -1;
   if (requested == RP_MFMA32) return mfma_ok ? RP_MFMA32 : -1;
   if (requested == RP_TILE) return tile_ok ? RP_TILE : -1;
   if (requested == RP_SCAN) return RP_SCAN;
@@ -1010,7 +1008,7 @@ int rank_impl(const kge_model_desc* m, int32_t mode, const int64_t* queries, int
   const bool reuse = (path & KGE_RANK_REUSE_TABLE) != 0;
   const bool ftab = (path & KGE_RANK_FILTER_TABLE) != 0;  // filt_off / filt_ids: the whole filter index
   path &= ~(KGE_RANK_REUSE_TABLE | KGE_RANK_STAGE_LIST | KGE_RANK_FILTER_TABLE);
-  if (path < RP_AUTO || path > RP_MFMA16) return KGE_ERR_ARG;
+  if (path < RP_AUTO || path > RP_MFMA32) return KGE_ERR_ARG;
   if (nq == 0) return KGE_OK;
   if (nq > 65535) return KGE_ERR_DIM;  // the bitmap launch puts queries on grid.y
   const int rp = rank_path(m, path);
@@ -1068,10 +1066,8 @@ int rank_impl(const kge_model_desc* m, int32_t mode, const int64_t* queries, int
   // the split-bf16 tile's error bound in units of u·‖q‖·max‖e‖ (kge_rank_mfma.hip): splitting
   // residuals and the final add 513.2, the dropped lo·lo products 256·(1 + 2^-8)^2 = 258.1, the
   // slab's three chained MFMAs 97.6, the running sum 1.02·nslab
-  const int64_t xns = xsplit_nslab(m->entity_dim, 0);
-  ra.fast_u = (rp == RP_MFMA)     ? (float)(513.2 + 258.1 + 97.6 + 1.02 * xns)
-              : (rp == RP_MFMA16) ? (float)(513.2 + 258.1 + 195.1 + 1.02 * (xsplit_nslab(m->entity_dim, 1) / 2))
-                                  : 0.f;
+  const int64_t xns = xsplit_nslab(m->entity_dim);
+  ra.fast_u = (rp != RP_MFMA) ? 0.f : (float)(513.2 + 258.1 + 97.6 + 1.02 * xns);
   if (stage == RS_ARGS) return launch_status(ops.rank_ref(mode, 3, ra, s));
   EmitArgs ea;
   ea.gt = w.gt; ea.eq = w.eq; ea.gtx = w.gtx; ea.eqx = w.eqx; ea.ucnt = w.ucnt; ea.true_id = w.true_id;
@@ -1094,7 +1090,7 @@ int rank_impl(const kge_model_desc* m, int32_t mode, const int64_t* queries, int
     // says this workspace already holds them for this table (k_rank_tag)
     const bool need_stats = (m->model == KGE_DISTMULT || m->model == KGE_COMPLEX || m->model == KGE_PROTATE);
     st = launch_status(launch_rank_tag(w.tag, m->entity_embedding, m->nentity, m->entity_dim, reuse ? 1 : 0,
-                                       need_stats ? 1 : 0, rp == RP_MFMA ? 1 : (rp == RP_MFMA16 ? 2 : 0), s));
+                                       need_stats ? 1 : 0, rp == RP_MFMA ? 1 : 0, s));
     if (st) return st;
     if (need_stats) {
       st = launch_status(launch_table_stats(m->entity_embedding, m->nentity, m->entity_dim, w.stats, s, w.tag + 5));
@@ -1109,12 +1105,11 @@ int rank_impl(const kge_model_desc* m, int32_t mode, const int64_t* queries, int
     // split-bf16 path: s_true in the reference's order after the window
     // (k_rank_true_ref, rows of ≤ 1024 floats: its LDS); wider rows take the
     // tile's own gather mode here (the window then covers two fast scores)
-    const bool true_ref = (rp == RP_MFMA && ((m->entity_dim + 3) & ~3) <= 1024) || rp == RP_MFMA16;
-    if (rp == RP_MFMA || rp == RP_MFMA16) {
-      const int l16 = rp == RP_MFMA16 ? 1 : 0;
-      st = launch_status(launch_split_bf16(w.q, nq, m->entity_dim, w.qs, s, nullptr, l16));
+    const bool true_ref = rp == RP_MFMA && ((m->entity_dim + 3) & ~3) <= 1024;
+    if (rp == RP_MFMA) {
+      st = launch_status(launch_split_bf16(w.q, nq, m->entity_dim, w.qs, s));
       if (!st)
-        st = launch_status(launch_split_bf16(m->entity_embedding, m->nentity, m->entity_dim, w.es, s, w.tag + 6, l16));
+        st = launch_status(launch_split_bf16(m->entity_embedding, m->nentity, m->entity_dim, w.es, s, w.tag + 6));
       if (!st && !true_ref)
         st = launch_status(launch_rank_mfma_x(1, w.qs, w.es, nq, m->nentity, m->entity_dim, w.true_id, w.s_true,
                                               w.bits, w.gt, win, s));
@@ -1134,10 +1129,7 @@ int rank_impl(const kge_model_desc* m, int32_t mode, const int64_t* queries, int
     }
     // 5. fast counting pass: clear cases counted, near-ties listed
     g_rank_timer.mark(s);  // (rank timer) 1: fast pass begins
-    if (rp == RP_MFMA16) {
-      st = launch_status(launch_rank_mfma_x16(w.qs, w.es, nq, m->nentity, m->entity_dim, w.true_id, w.s_true,
-                                              w.bits, w.gt, win, s));
-    } else if (rp == RP_MFMA) {
+    if (rp == RP_MFMA) {
       st = launch_status(launch_rank_mfma_x(0, w.qs, w.es, nq, m->nentity, m->entity_dim, w.true_id, w.s_true,
                                             w.bits, w.gt, win, s));
     } else if (rp == RP_MFMA32) {

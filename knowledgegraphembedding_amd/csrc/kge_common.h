@@ -26,15 +26,12 @@ int launch_rank_mfma(int gather, const float* q, const float* ent, int64_t nq, i
                      const int64_t* true_id, float* s_true, const uint32_t* bits, int32_t* gt, const RankWin& win,
                      hipStream_t s);
 // split-bf16 MFMA tile (path "mfma"): operands split once per call into bf16 hi | lo pieces
-int64_t xsplit_nslab(int K, int pairs);  // 16-k slabs per row (pairs: rounded up to even, the 16x16x32 tile's layout)
+int64_t xsplit_nslab(int K);
 // (three bf16 MFMAs per fp32 product: the lo·lo products are dropped, +258.1·u·P
 // on the error bound — kge_rank_mfma.hip, kge_capi.hip rank_impl)
 int64_t xsplit_elems(int64_t rows, int K);
 int launch_split_bf16(const float* src, int64_t rows, int K, uint16_t* dst, hipStream_t s,
-                      const int64_t* skip = nullptr, int layout16 = 0);
-int launch_rank_mfma_x16(const uint16_t* qs, const uint16_t* es, int64_t nq, int64_t E, int K,
-                         const int64_t* true_id, float* s_true, const uint32_t* bits, int32_t* gt, const RankWin& win,
-                         hipStream_t s);
+                      const int64_t* skip = nullptr);
 int launch_rank_mfma_x(int gather, const uint16_t* qs, const uint16_t* es, int64_t nq, int64_t E, int K,
                        const int64_t* true_id, float* s_true, const uint32_t* bits, int32_t* gt, const RankWin& win,
                        hipStream_t s);

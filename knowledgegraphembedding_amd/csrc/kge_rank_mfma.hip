@@ -368,8 +368,7 @@ __device__ __forceinline__ uint32_t bf16_rne(float x) {
 // as 256 contiguous bytes and, per slab, the 8 rows' hi (lo) pieces are
 // written as 256 contiguous bytes.
 __global__ __launch_bounds__(256) void k_split_bf16(const float* __restrict__ src, int64_t rows, int K, int nslab,
-                                                    int64_t nrb, uint16_t* __restrict__ dst, const int64_t* skip,
-                                                    int swap) {
+                                                    int64_t nrb, uint16_t* __restrict__ dst, const int64_t* skip) {
   if (skip && *skip) return;  // the workspace already holds this table's split (k_rank_tag)
   const int64_t wg = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
   const int lane = threadIdx.x & 63;
@@ -399,7 +398,7 @@ __global__ __launch_bounds__(256) void k_split_bf16(const float* __restrict__ sr
   const uint4 vl = {lo[0] | (lo[1] << 16), lo[2] | (lo[3] << 16), lo[4] | (lo[5] << 16), lo[6] | (lo[7] << 16)};
   const int64_t rb = row >> 7;
   uint16_t* o = dst + ((rb * nslab + (kg >> 1)) * 2) * XS_PIECE + (row & 127) * XS_BK +
-                ((kg & 1) ^ (swap ? (int)((row >> 3) & 1) : 0)) * 8;
+                ((kg & 1) ^ (int)((row >> 3) & 1)) * 8;
   *reinterpret_cast<uint4*>(o) = vh;
   *reinterpret_cast<uint4*>(o + XS_PIECE) = vl;
 }
@@ -450,7 +449,10 @@ __device__ __forceinline__ bool xcd_tile(const XArgs& a, int& x, int& y) {
 // numbers in DESIGN §5 and profiles/r04/rank/: a separate correction
 // accumulator, a 4-stage ring at two workgroups per CU, 64 × 32 per wave, a
 // 256-candidate 8-wave tile with 4-6 ring stages, a persistent ring, keeping
-// the lo·lo product.
+// the lo·lo product, and (round 5) the same tile on v_mfma_f32_16x16x32_bf16
+// (each MFMA over a 32-k slab pair, 4 × 4 blocks of 16 × 16 per wave, 199
+// VGPRs, two workgroups per CU: DistMult 399-404 against 374-375 µs, ComplEx
+// 705-714 against 711-712, profiles/r05/rank/ab_tile_16x16x32_rejected.txt).
 // s_waitcnt vmcnt(n) for the DMA counts of the ring (n = younger slabs × CPW)
 __device__ __forceinline__ void wait_vmcnt_dma(int n) {
   switch (n) {
@@ -690,163 +692,6 @@ __global__ __launch_bounds__(256, 3) void k_rank_mfma_x(XArgs a) {
   if (t < X::BQ && arow[t] >= 0 && cgt[t]) atomicAdd(&a.gt[q0 + t], cgt[t]);
 }
 
-// Experiment (path "mfma16"): the same counting tile on v_mfma_f32_16x16x32_bf16
-// (MI355X_MICROARCH.md: ≈1.12-1.15× the FLOP/s of 32x32x16 with LDS-fed
-// operands).  Each MFMA spans two 16-k slabs (a 32-k "pair"); the ring holds
-// four slab stages, a pair computed while the next pair's DMA is in flight.
-// Per wave 64 candidates × 64 queries as 4 × 4 blocks of 16 × 16 (C/D: col =
-// lane & 15 = query, row = 4·(lane >> 4) + reg = candidate); A/B fragments:
-// lane l holds row l & 15, k = 8·(l >> 4) .. +7 of the pair, i.e. slab
-// (l >> 5), k-half ((l >> 4) & 1) — read from an UNSWAPPED split layout
-// (every 16-lane ds_read_b128 group then covers all 64 banks).  Error: each
-// chained MFMA sums 32 products (≤ 64u each), the running sum takes one add
-// per pair: fast_u = 513.2 + 258.1 + 195.1 + 1.02·npair.
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-__global__ __launch_bounds__(256, 2) void k_rank_mfma_x16(XArgs a) {
-  constexpr int NST = 4, CPW = 4;
-  constexpr int STAGE = 16 * 512;  // bf16 per slab stage: E hi | lo (4 KB each), Q hi | lo (4 KB each)
-  __shared__ __attribute__((aligned(16))) uint16_t smem[NST * STAGE + 128 * 4 * 2 + 128 * 2 * 3];
-  int64_t* arow = reinterpret_cast<int64_t*>(smem + NST * STAGE);
-  float* sts = reinterpret_cast<float*>(arow + 128);
-  float* sdl = sts + 128;
-  int32_t* cgt = reinterpret_cast<int32_t*>(sdl + 128);
-  const int t = threadIdx.x, lane = t & 63, w = wave_id();
-  const int wm = w >> 1, wn = w & 1;
-  int tx = 0, ty = 0;
-  if (!xcd_tile(a, tx, ty)) return;  // (block-uniform)
-  const int64_t q0 = (int64_t)ty * 128;
-  const int64_t e0 = (int64_t)tx * 128;
-  if (t < 128) {
-    const int64_t q = q0 + t;
-    const bool in = q < a.nq;
-    arow[t] = in ? q : -1;
-    sts[t] = in ? a.s_true[q] : 0.f;
-    sdl[t] = in ? a.win.delta[q] : 0.f;
-    cgt[t] = 0;
-  }
-  __syncthreads();
-  const auto rq = buf_rsrc(a.qs, a.qs_bytes);
-  const auto re = buf_rsrc(a.es, a.es_bytes);
-  const int nslab = a.nslab;  // even
-  constexpr uint32_t SLAB_BYTES = 2u * (2u * XS_PIECE);
-  uint32_t off0[CPW];
-#pragma unroll
-  for (int k = 0; k < CPW; ++k) {
-    const int c = CPW * w + k;
-    if (c < 8) {
-      const int piece = (c >> 2) & 1, sub = c & 3;
-      off0[k] = (uint32_t)(((int64_t)tx * nslab * 2 + piece) * (2 * XS_PIECE) + sub * 1024 + lane * 16);
-    } else {
-      const int cc = c - 8, piece = cc / 4, sub = cc % 4;
-      off0[k] = (uint32_t)(((int64_t)ty * nslab * 2 + piece) * (2 * XS_PIECE) + sub * 1024 + lane * 16);
-    }
-  }
-  auto issue = [&](int sl, int st) {
-    uint16_t* base = smem + st * STAGE;
-#pragma unroll
-    for (int k = 0; k < CPW; ++k) {
-      const int c = CPW * w + k;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(c < 8 ? re : rq,
-                                               (__attribute__((address_space(3))) void*)(base + c * 512), 16,
-                                               off0[k] + (uint32_t)sl * SLAB_BYTES, 0, 0, 0);
-    }
-  };
-  f32x4 run[4][4], mprev[4][4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) run[i][j] = mprev[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
-  const int r16 = lane & 15, sh = lane >> 5, kh = (lane >> 4) & 1;
-  const int wq0 = wn * 64;
-  const bool live = q0 + wq0 < a.nq && e0 + wm * 64 < a.E;
-  uint32_t exw[4][2];  // [query block j][candidate word]
-#pragma unroll
-  for (int j = 0; j < 4; ++j)
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int64_t q = q0 + wq0 + j * 16 + r16;
-      const int64_t widx = (e0 >> 5) + wm * 2 + i;
-      const int64_t cbase = e0 + wm * 64 + i * 32;
-      uint32_t word = (q < a.nq && widx < a.W) ? a.fbits[q * a.W + widx] : ~0u;
-      const int64_t valid = a.E - cbase;
-      if (valid < 32) word |= (valid <= 0) ? ~0u : (~0u << valid);
-      exw[j][i] = word;
-    }
-  issue(0, 0);
-  if (1 < nslab) issue(1, 1);
-  for (int sl = 0; sl < nslab; sl += 2) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA of the pair has landed
-    __builtin_amdgcn_s_barrier();                      // ... every wave's; the previous pair's reads are done
-    if (sl + 2 < nslab) {
-      issue(sl + 2, (sl + 2) % NST);
-      issue(sl + 3, (sl + 3) % NST);
-    }
-    if (!live) continue;
-    const uint16_t* S0 = smem + ((sl + sh) % NST) * STAGE;  // this lane's slab of the pair
-    bf16x8 eh[4], el[4], qh[4], ql[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int row = wm * 64 + i * 16 + r16;
-      eh[i] = *reinterpret_cast<const bf16x8*>(S0 + row * XS_BK + kh * 8);
-      el[i] = *reinterpret_cast<const bf16x8*>(S0 + XS_PIECE + row * XS_BK + kh * 8);
-    }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int row = wq0 + j * 16 + r16;
-      qh[j] = *reinterpret_cast<const bf16x8*>(S0 + 2 * XS_PIECE + row * XS_BK + kh * 8);
-      ql[j] = *reinterpret_cast<const bf16x8*>(S0 + 3 * XS_PIECE + row * XS_BK + kh * 8);
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        run[i][j] += mprev[i][j];
-        mprev[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(eh[i], qh[j], zero, 0, 0, 0);
-        mprev[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(eh[i], ql[j], mprev[i][j], 0, 0, 0);
-        mprev[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(el[i], qh[j], mprev[i][j], 0, 0, 0);
-      }
-  }
-  // counting: lane holds query col wq0 + 16·j + (lane & 15), candidates
-  // wm·64 + 16·i + 4·(lane >> 4) + r
-  const int g4 = lane >> 4;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int n = wq0 + j * 16 + r16;
-    const int64_t q = arow[n];
-    const float st = sts[n], dlt = sdl[n];
-    int g = 0;
-    uint32_t near = 0;  // bit 4·i + r
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const f32x4 acc = run[i][j] + mprev[i][j];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int cl = (i & 1) * 16 + g4 * 4 + r;  // bit in candidate word i >> 1
-        const float sc = ((exw[j][i >> 1] >> cl) & 1u) ? -__builtin_inff() : acc[r];
-        const float diff = sc - st;
-        g += (diff > dlt) ? 1 : 0;
-        near |= (__builtin_fabsf(diff) <= dlt) ? (1u << (4 * i + r)) : 0u;
-      }
-    }
-    if (__builtin_amdgcn_ballot_w64(near != 0u)) {
-      while (near) {
-        const int b = __builtin_ctz(near);
-        near &= near - 1u;
-        const int i = b >> 2, r = b & 3;
-        const int idx = atomicAdd(&a.win.ucnt[q], 1);
-        if (idx < a.win.cap)
-          a.win.ulist[q * (int64_t)a.win.cap + idx] = (int32_t)(e0 + wm * 64 + i * 16 + g4 * 4 + r);
-      }
-    }
-    g += __shfl_xor(g, 16);
-    g += __shfl_xor(g, 32);
-    if (g4 == 0 && q >= 0 && g) atomicAdd(&cgt[n], g);
-  }
-  __syncthreads();
-  if (t < 128 && arow[t] >= 0 && cgt[t]) atomicAdd(&a.gt[q0 + t], cgt[t]);
-}
-
 }  // namespace
 
 int launch_filter_bits(const int64_t* filt_off, const int64_t* filt_ids, const int64_t* true_id, int64_t nq,
@@ -900,37 +745,14 @@ int launch_rank_mfma(int gather, const float* q, const float* ent, int64_t nq, i
 }
 
 // split-bf16 tile: buffer sizes and launchers (path "mfma")
-int64_t xsplit_nslab(int K, int pairs) {
-  const int64_t n = (K + XS_BK - 1) / XS_BK;
-  return pairs ? (n + 1) & ~(int64_t)1 : n;
-}
-// (the buffers are sized for the pair layout, ≥ the single-slab one)
-int64_t xsplit_elems(int64_t rows, int K) { return ((rows + 127) / 128) * 128 * xsplit_nslab(K, 1) * XS_BK * 2; }
+int64_t xsplit_nslab(int K) { return (K + XS_BK - 1) / XS_BK; }
+int64_t xsplit_elems(int64_t rows, int K) { return ((rows + 127) / 128) * 128 * xsplit_nslab(K) * XS_BK * 2; }
 
-int launch_split_bf16(const float* src, int64_t rows, int K, uint16_t* dst, hipStream_t s, const int64_t* skip,
-                      int layout16) {
-  const int64_t nrb = (rows + 127) / 128, nslab = xsplit_nslab(K, layout16);
+int launch_split_bf16(const float* src, int64_t rows, int K, uint16_t* dst, hipStream_t s, const int64_t* skip) {
+  const int64_t nrb = (rows + 127) / 128, nslab = xsplit_nslab(K);
   const int64_t waves = nrb * 16 * ((nslab * XS_BK + 63) / 64);  // 8 rows × 64 k each
   hipLaunchKernelGGL(k_split_bf16, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s, src, rows, K, (int)nslab,
-                     nrb, dst, skip, layout16 ? 0 : 1);
-  return (int)hipGetLastError();
-}
-
-int launch_rank_mfma_x16(const uint16_t* qs, const uint16_t* es, int64_t nq, int64_t E, int K,
-                         const int64_t* true_id, float* s_true, const uint32_t* bits, int32_t* gt, const RankWin& win,
-                         hipStream_t s) {
-  XArgs a;
-  a.qs = qs; a.es = es; a.nq = nq; a.E = E; a.nslab = (int)xsplit_nslab(K, 1);
-  const uint64_t qb = (uint64_t)xsplit_elems(nq, K) * 2u, eb = (uint64_t)xsplit_elems(E, K) * 2u;
-  if (qb >= XS_OOB || eb >= XS_OOB) return -1;
-  a.qs_bytes = (uint32_t)qb; a.es_bytes = (uint32_t)eb;
-  a.true_id = true_id; a.s_true = s_true; a.fbits = bits; a.W = (E + 31) / 32; a.gt = gt; a.win = win;
-  a.gx = (int)((E + 127) / 128);
-  a.gy = (int)((nq + 127) / 128);
-  const int64_t tile_bytes = (int64_t)128 * a.nslab * XS_BK * 4;
-  a.group = (int)std::max<int64_t>(1, (2 << 20) / tile_bytes);
-  const int64_t per_xcd = (int64_t)((a.gx + 7) / 8) * a.gy;
-  hipLaunchKernelGGL(k_rank_mfma_x16, dim3((unsigned)(8 * per_xcd)), dim3(256), 0, s, a);
+                     nrb, dst, skip);
   return (int)hipGetLastError();
 }
 
@@ -938,7 +760,7 @@ int launch_rank_mfma_x(int gather, const uint16_t* qs, const uint16_t* es, int64
                        const int64_t* true_id, float* s_true, const uint32_t* bits, int32_t* gt, const RankWin& win,
                        hipStream_t s) {
   XArgs a;
-  a.qs = qs; a.es = es; a.nq = nq; a.E = E; a.nslab = (int)xsplit_nslab(K, 0);
+  a.qs = qs; a.es = es; a.nq = nq; a.E = E; a.nslab = (int)xsplit_nslab(K);
   const uint64_t qb = (uint64_t)xsplit_elems(nq, K) * 2u, eb = (uint64_t)xsplit_elems(E, K) * 2u;
   if (qb >= XS_OOB || eb >= XS_OOB) return -1;  // 32-bit buffer offsets, XS_OOB reads zeros
   a.qs_bytes = (uint32_t)qb; a.es_bytes = (uint32_t)eb;
@@ -1060,12 +882,12 @@ __global__ void k_rank_tag(int64_t* tag, const float* ent, int64_t E, int Le, in
   const bool match = reuse && tag[0] == (int64_t)(uintptr_t)ent && tag[1] == E && tag[2] == Le;
   const int64_t sv = match ? tag[3] : 0, xv = match ? tag[4] : 0;
   tag[5] = (need_stats && sv) ? 1 : 0;
-  tag[6] = (need_split && xv == need_split) ? 1 : 0;  // need_split: the split layout (1: 32x32 tile, 2: 16x16)
+  tag[6] = (need_split && xv) ? 1 : 0;
   tag[0] = (int64_t)(uintptr_t)ent;
   tag[1] = E;
   tag[2] = Le;
   tag[3] = need_stats ? 1 : sv;
-  tag[4] = need_split ? need_split : xv;
+  tag[4] = need_split ? 1 : xv;
   tag[8] = tag[9] = tag[10] = 0;  // any ranking call voids pRotatE's list tag (its list stage rewrites it)
 }
 

@@ -395,7 +395,7 @@ def adam_step(param: torch.Tensor, grad: torch.Tensor, exp_avg: torch.Tensor, ex
     )
 
 
-RANK_PATHS = {"auto": 0, "mfma": 1, "tile": 2, "scan": 3, "mfma32": 4, "mfma16": 5}
+RANK_PATHS = {"auto": 0, "mfma": 1, "tile": 2, "scan": 3, "mfma32": 4}
 
 
 def reference_rotation(relation: torch.Tensor, embedding_range: float) -> torch.Tensor:

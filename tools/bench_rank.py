@@ -41,8 +41,6 @@ def rank_path(name, K, path="auto"):
     """Which fast pass kge_rank_filtered_ex runs (kge_capi.hip rank_path)."""
     red = K // 2 if name in ("RotatE", "ComplEx") else K
     mfma_ok = name in ("DistMult", "ComplEx") and K % 4 == 0
-    if path == "mfma16":
-        return "mfma-split-bf16-16x16x32"
     if path == "mfma" or (path == "auto" and name in ("DistMult", "ComplEx")):
         return "mfma-split-bf16"
     if path == "mfma32" or (path == "auto" and mfma_ok):
@@ -57,7 +55,7 @@ def main():
     ap.add_argument("--models", nargs="+", default=["DistMult", "ComplEx"])
     ap.add_argument("-d", "--hidden_dim", type=int, default=500)
     ap.add_argument("--reps", type=int, default=3)
-    ap.add_argument("--path", default="auto", choices=("auto", "mfma", "mfma16", "mfma32", "tile", "scan"))
+    ap.add_argument("--path", default="auto", choices=("auto", "mfma", "mfma32", "tile", "scan"))
     ap.add_argument("--cpu-sample", type=int, default=0, help="queries timed through the CPU oracle (0: skip)")
     ap.add_argument("--shape", default="wn18rr", choices=sorted(SHAPES))
     ap.add_argument("--gamma", type=float, default=12.0)
@@ -102,7 +100,7 @@ def main():
                "listed_per_query": float(np.mean(np.concatenate([lh, lt])))}
         if res["path"].startswith("mfma-split-bf16"):
             pad = lambda x, m: -(-x // m) * m  # noqa: E731
-            kp = pad(K, 32 if res["path"].endswith("16x16x32") else 16)
+            kp = pad(K, 16)
             issued = 2.0 * 3 * 2 * pad(NTEST, 128) * pad(E, 128) * kp  # three bf16 products per fp32 one
             res["roofline"] = {"bound": "mfma", "achieved": issued / dt / 1e12, "peak": BF16_PEAK_TF,
                                "unit": "TFLOP/s", "frac": issued / dt / 1e12 / BF16_PEAK_TF,
