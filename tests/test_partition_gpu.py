@@ -166,10 +166,12 @@ def test_row_partition_yago3_10_shape(world, exchange):
 
     def close(got, want, what):
         # an element whose gradient sums to ~0 can take Adam's ±lr step with
-        # the other sign when the two paths round the sum differently: allow
-        # such elements (≤ 1e-5 of them), never a step larger than 2 lr
+        # the other sign when the two paths round the sum differently (world
+        # 8's query shipping sums the relation gradient over 8 shards: one such
+        # element of the 37,000 relation entries, r05d): allow such elements
+        # (≤ 1e-5 of them, at least 2), never a step larger than 2 lr
         bad = np.abs(got - want) > 1e-5 * np.abs(want) + 2e-7
-        assert bad.sum() <= 1e-5 * got.size, (what, int(bad.sum()))
+        assert bad.sum() <= max(2, 1e-5 * got.size), (what, int(bad.sum()))
         assert np.abs(got - want).max() <= 2 * 2 * 1e-4 + 1e-6, what
 
     for rank in range(world):
