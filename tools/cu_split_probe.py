@@ -13,6 +13,13 @@ real one also waits for each gradient chunk before its Adam chunk).  The
 fused pass (gradient + Adam, one launch) is timed on all CUs beside them.
 
     python tools/cu_split_probe.py [--reps 20]
+
+Its gather_* columns (0.044 ms on 64 or 256 CUs, profiles/r05/train/
+cu_split_probe.json) are NOT the kernel's time: the same ENTITY-phase launch
+runs 0.140-0.165 ms in every rocprofv3 trace (in the step, repeated, after a
+cache flush: tools/entity_gather_probe.py, profiles/r05/train/), so the
+concurrent / pipeline rows built on it are not evidence either.  The adam_*
+columns agree with the traced k_adam (0.145-0.149 ms).
 """
 import argparse
 import ctypes
@@ -142,6 +149,44 @@ def main():
         t1.record()
         t1.synchronize()
         out[f"concurrent_gather{ng}_adam{ncu - ng}_ms"] = t0.elapsed_time(t1) / a.reps
+    # the production shape of a split: the gradient pass in entity-row chunks
+    # on the gather CUs, each chunk's Adam on the stream CUs behind an event
+    pm, gm = model.entity_embedding.detach(), ge
+    mm, vm = torch.zeros_like(pm), torch.zeros_like(pm)
+
+    def pipeline(ng, chunks, reps):
+        cg = [int(i * ncu / ng) for i in range(ng)]
+        ca = sorted(set(range(ncu)) - set(cg))
+        sg, sa = masked_stream(cg, ncu), masked_stream(ca, ncu)
+        step = -(-E // chunks)
+        bounds = [(e0, min(E, e0 + step)) for e0 in range(0, E, step)]
+        evs = [torch.cuda.Event() for _ in bounds]
+        torch.cuda.synchronize()
+        t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        t0.record()
+        for _ in range(reps):
+            ev0 = torch.cuda.Event()
+            ev0.record()
+            sg.wait_event(ev0)
+            sa.wait_event(ev0)
+            for (e0, e1), ev in zip(bounds, evs):
+                with torch.cuda.stream(sg):
+                    ops.train_step_grads(desc, "tail-batch", pos, neg, w, dev, phases=_lib.PHASE_ENTITY,
+                                         entity_range=(e0, e1), **kw)
+                    ev.record()
+                sa.wait_event(ev)
+                with torch.cuda.stream(sa):
+                    ops.adam_step(pm[e0:e1], gm[e0:e1], mm[e0:e1], vm[e0:e1], step=1, lr=1e-4, beta1=0.9,
+                                  beta2=0.999, eps=1e-8)
+            torch.cuda.current_stream().wait_stream(sg)
+            torch.cuda.current_stream().wait_stream(sa)
+        t1.record()
+        t1.synchronize()
+        return t0.elapsed_time(t1) / reps
+
+    for ng in (160, 192, 224):
+        for chunks in (4, 8):
+            out[f"pipeline_gather{ng}_adam{ncu - ng}_chunks{chunks}_ms"] = pipeline(ng, chunks, a.reps)
     print(json.dumps(out), flush=True)
 
 
