@@ -619,6 +619,12 @@ __global__ __launch_bounds__(256, 3) void k_rank_mfma_x(XArgs a) {
     // the running sum takes the PREVIOUS slab's chain (long done: an add
     // right behind the MFMA it reads stalls the wave ~40 cycles), then this
     // slab's hi·hi, hi·lo and lo·hi MFMAs chain from zero
+    // the MFMA block at raised wave priority: with three waves per SIMD on one
+    // matrix core, a wave that reached its MFMAs issues them ahead of the
+    // others' fragment reads and DMA issue (DistMult 385 -> 378-387 us, ComplEx
+    // 735 -> 716-717 us, alternated; the reads / DMA raised instead: 383 / 727-732,
+    // profiles/r05/rank/ab_setprio.txt)
+    __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -628,6 +634,7 @@ __global__ __launch_bounds__(256, 3) void k_rank_mfma_x(XArgs a) {
         mprev[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(eh[i], ql[j], mprev[i][j], 0, 0, 0);
         mprev[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(el[i], qh[j], mprev[i][j], 0, 0, 0);
       }
+    __builtin_amdgcn_s_setprio(0);
   }
   f32x16 acc[2][TQ];
 #pragma unroll
