@@ -934,6 +934,7 @@ struct RankWs {
   int32_t *gt, *eq, *gtx, *eqx, *ucnt, *done, *ulist;
   uint32_t* bits;
   uint16_t *qs, *es;  // split-bf16 operands (DistMult / ComplEx)
+  float *qph, *eph;   // pRotatE's phase tables for the register tile ([rows][K][2])
 };
 RankWs carve_rank(void* ws, const kge_model_desc* m, int64_t nq, size_t* bytes) {
   Carver c(ws);
@@ -945,7 +946,11 @@ RankWs carve_rank(void* ws, const kge_model_desc* m, int64_t nq, size_t* bytes) 
   // split-bf16 operands: only where the split tile can run (rank_path's x_ok)
   const bool xs = rank_path(m, RP_MFMA) == RP_MFMA;
   w.es = c.take<uint16_t>(xs ? xsplit_elems(m->nentity, m->entity_dim) : 0);
+  // pRotatE's phase tables: only where its register tile can run
+  const bool ph = m->model == KGE_PROTATE && rank_path(m, RP_TILE) == RP_TILE;
+  w.eph = c.take<float>(ph ? 2 * m->nentity * (int64_t)m->entity_dim : 0);
   w.qs = c.take<uint16_t>(xs ? xsplit_elems(nq, m->entity_dim) : 0);
+  w.qph = c.take<float>(ph ? 2 * nq * (int64_t)m->entity_dim : 0);
   w.q = c.take<float>(nq * (int64_t)m->entity_dim);
   w.qref = c.take<float>(nq * (int64_t)m->entity_dim);
   w.s_true = c.take<float>(nq);
@@ -1089,8 +1094,15 @@ int rank_impl(const kge_model_desc* m, int32_t mode, const int64_t* queries, int
     // the table's statistics and split operands: reused only where the tag
     // says this workspace already holds them for this table (k_rank_tag)
     const bool need_stats = (m->model == KGE_DISTMULT || m->model == KGE_COMPLEX || m->model == KGE_PROTATE);
+    // the derived table: split-bf16 operands (kind 1) or pRotatE's phase table
+    // (kind 2, tagged with its divisor's bits)
+    const bool prot_tile = m->model == KGE_PROTATE && rp == RP_TILE;
+    const float kappa = a.c.kappa_p;
+    int64_t kbits = 0;
+    memcpy(&kbits, &kappa, sizeof(kappa));
     st = launch_status(launch_rank_tag(w.tag, m->entity_embedding, m->nentity, m->entity_dim, reuse ? 1 : 0,
-                                       need_stats ? 1 : 0, rp == RP_MFMA ? 1 : 0, s));
+                                       need_stats ? 1 : 0, rp == RP_MFMA ? 1 : (prot_tile ? 2 : 0),
+                                       prot_tile ? kbits : 0, s));
     if (st) return st;
     if (need_stats) {
       st = launch_status(launch_table_stats(m->entity_embedding, m->nentity, m->entity_dim, w.stats, s, w.tag + 5));
@@ -1102,6 +1114,12 @@ int rank_impl(const kge_model_desc* m, int32_t mode, const int64_t* queries, int
     ta.nq = nq; ta.E = m->nentity; ta.Le = m->entity_dim; ta.K = K;
     ta.c = a.c; ta.true_id = w.true_id; ta.s_true = w.s_true;
     ta.fbits = w.bits; ta.W = a.W; ta.gt = w.gt; ta.win = win;
+    ta.qph = w.qph; ta.eph = w.eph;
+    if (prot_tile) {
+      st = launch_status(launch_prot_phase(w.q, nq, K, 0.f, 0, w.qph, s));
+      if (!st) st = launch_status(launch_prot_phase(m->entity_embedding, m->nentity, K, kappa, 1, w.eph, s, w.tag + 6));
+      if (st) return st;
+    }
     // split-bf16 path: s_true in the reference's order after the window
     // (k_rank_true_ref, rows of ≤ 1024 floats: its LDS); wider rows take the
     // tile's own gather mode here (the window then covers two fast scores)

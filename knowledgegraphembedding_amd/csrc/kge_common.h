@@ -39,8 +39,11 @@ constexpr int TS_BLOCKS = 1024;  // k_table_stats grid bound: stats holds 2 + 2Â
 int launch_table_stats(const float* ent, int64_t E, int Le, float* stats, hipStream_t s,
                        const int64_t* skip = nullptr);
 // the ranking workspace's table tag (KGE_RANK_REUSE_TABLE; kge_rank_mfma.hip k_rank_tag)
-int launch_rank_tag(int64_t* tag, const float* ent, int64_t E, int Le, int reuse, int need_stats, int need_split,
-                    hipStream_t s);
+int launch_rank_tag(int64_t* tag, const float* ent, int64_t E, int Le, int reuse, int need_stats, int split_kind,
+                    int64_t split_param, hipStream_t s);
+// pRotatE's (cos, sin) / (sin, cos) phase table for the register tile ([rows][K][2]; kge_rank_mfma.hip)
+int launch_prot_phase(const float* src, int64_t rows, int K, float kappa, int ent, float* dst, hipStream_t s,
+                      const int64_t* skip = nullptr);
 int launch_filter_bits_tab(const int64_t* queries, int head, const int64_t* tab, const int64_t* vals,
                            const int64_t* true_id, int64_t nq, int64_t E, int64_t R, uint32_t* bits, int32_t* err,
                            hipStream_t s);

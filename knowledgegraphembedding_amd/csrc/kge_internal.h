@@ -272,6 +272,8 @@ struct TileArgs {
   int64_t W;
   int32_t* gt;             // [nq]
   RankWin win;
+  const float* qph;        // pRotatE: [nq, K, 2] (sin, cos) of q's phase sums (launch_prot_phase)
+  const float* eph;        // pRotatE: [E, K, 2] (cos, sin) of the candidate phases
 };
 
 struct ModelOps {

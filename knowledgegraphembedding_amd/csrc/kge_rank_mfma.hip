@@ -763,6 +763,48 @@ int launch_split_bf16(const float* src, int64_t rows, int K, uint16_t* dst, hipS
   return (int)hipGetLastError();
 }
 
+// pRotatE's phase table for the register tile (k_rank_tile<PROTATE>): per
+// element the (cos, sin) pair of the candidate phase x / kappa (entity rows,
+// ent = 1; the true division the tile used to evaluate per block,
+// model.py:245-246) or the (sin, cos) pair of the query's phase sum x (q rows,
+// ent = 0), as [row][K][2] floats.  sincosf here is the same library call the
+// tile's staging made, so the tile's products — and ranks — are unchanged; the
+// tile no longer evaluates 8 sincos per thread and slab for every (query tile,
+// candidate tile) pair (wn18rr: 640 times per element).  One thread per 4
+// elements; K % 4 == 0 (the tile's own condition).
+__global__ __launch_bounds__(256) void k_prot_phase(const float* __restrict__ src, int64_t rows, int K, float kappa,
+                                                    int ent, float* __restrict__ dst, const int64_t* skip) {
+  if (skip && *skip) return;  // the workspace already holds this table's phases (k_rank_tag)
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t kq = K / 4;
+  if (i >= rows * kq) return;
+  const int64_t row = i / kq;
+  const int k = (int)(i - row * kq) * 4;
+  const float4 x = *reinterpret_cast<const float4*>(src + row * K + k);
+  const float v[4] = {x.x, x.y, x.z, x.w};
+  float o[8];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    float sv, cv;
+    sincosf(ent ? v[u] / kappa : v[u], &sv, &cv);
+    o[2 * u] = ent ? cv : sv;
+    o[2 * u + 1] = ent ? sv : cv;
+  }
+  float4* d = reinterpret_cast<float4*>(dst + (row * K + k) * 2);
+  d[0] = make_float4(o[0], o[1], o[2], o[3]);
+  d[1] = make_float4(o[4], o[5], o[6], o[7]);
+}
+
+int launch_prot_phase(const float* src, int64_t rows, int K, float kappa, int ent, float* dst, hipStream_t s,
+                      const int64_t* skip) {
+  if (K % 4 != 0 || ((uintptr_t)src & 15) || ((uintptr_t)dst & 15)) return -1;
+  const int64_t n = rows * (K / 4);
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(k_prot_phase, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, src, rows, K, kappa, ent, dst,
+                     skip);
+  return (int)hipGetLastError();
+}
+
 int launch_rank_mfma_x(int gather, const uint16_t* qs, const uint16_t* es, int64_t nq, int64_t E, int K,
                        const int64_t* true_id, float* s_true, const uint32_t* bits, int32_t* gt, const RankWin& win,
                        hipStream_t s) {
@@ -876,31 +918,43 @@ int launch_table_stats(const float* ent, int64_t E, int Le, float* stats, hipStr
 }
 
 // The ranking workspace's table tag (KGE_RANK_REUSE_TABLE): tag = [entity
-// pointer, nentity, entity_dim, statistics valid, split valid, skip statistics,
-// skip split, -].  With reuse requested, the statistics / split operands a
+// pointer, nentity, entity_dim, statistics valid, derived-table valid, skip
+// statistics, skip derived table, derived-table kind], [8..10] pRotatE's list
+// tag, [11] the derived table's parameter.  The derived table is the split-bf16
+// operands (kind 1) or pRotatE's phase table (kind 2, parameter = the phase
+// divisor's bits).  With reuse requested, the statistics / derived table a
 // previous call left are reused only if that call ranked the same table
-// pointer and shape and actually wrote them (a scan- or tile-path call writes
-// no split; a DistMult call after a RotatE one finds no statistics); the tag
-// then describes what this call leaves behind.  One thread, stream-ordered
-// before the kernels that read the skip words.
+// pointer and shape and actually wrote them, of the same kind and parameter
+// (a scan-path call writes none; a DistMult call after a RotatE one finds no
+// statistics; a pRotatE call after a DistMult one on the same tensor finds a
+// split, not phases); the tag then describes what this call leaves behind.
+// One thread, stream-ordered before the kernels that read the skip words.
 __global__ void k_rank_tag(int64_t* tag, const float* ent, int64_t E, int Le, int reuse, int need_stats,
-                           int need_split) {
+                           int split_kind, int64_t split_param) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   const bool match = reuse && tag[0] == (int64_t)(uintptr_t)ent && tag[1] == E && tag[2] == Le;
-  const int64_t sv = match ? tag[3] : 0, xv = match ? tag[4] : 0;
+  const int64_t sv = match ? tag[3] : 0;
+  const int64_t xv = (match && tag[7] == split_kind && tag[11] == split_param) ? tag[4] : 0;
   tag[5] = (need_stats && sv) ? 1 : 0;
-  tag[6] = (need_split && xv) ? 1 : 0;
+  tag[6] = (split_kind && xv) ? 1 : 0;
   tag[0] = (int64_t)(uintptr_t)ent;
   tag[1] = E;
   tag[2] = Le;
   tag[3] = need_stats ? 1 : sv;
-  tag[4] = need_split ? 1 : xv;
+  if (split_kind) {
+    tag[4] = 1;
+    tag[7] = split_kind;
+    tag[11] = split_param;
+  } else if (!match) {
+    tag[4] = 0;
+  }
   tag[8] = tag[9] = tag[10] = 0;  // any ranking call voids pRotatE's list tag (its list stage rewrites it)
 }
 
-int launch_rank_tag(int64_t* tag, const float* ent, int64_t E, int Le, int reuse, int need_stats, int need_split,
-                    hipStream_t s) {
-  hipLaunchKernelGGL(k_rank_tag, dim3(1), dim3(64), 0, s, tag, ent, E, Le, reuse, need_stats, need_split);
+int launch_rank_tag(int64_t* tag, const float* ent, int64_t E, int Le, int reuse, int need_stats, int split_kind,
+                    int64_t split_param, hipStream_t s) {
+  hipLaunchKernelGGL(k_rank_tag, dim3(1), dim3(64), 0, s, tag, ent, E, Le, reuse, need_stats, split_kind,
+                     split_param);
   return (int)hipGetLastError();
 }
 

@@ -108,7 +108,7 @@ def test_rank_queries_both_directions_pipelined(name):
     assert np.array_equal(rt, rt1) and np.array_equal(tt, tt1)
 
 
-@pytest.mark.parametrize("name", ["DistMult", "ComplEx"])
+@pytest.mark.parametrize("name", ["DistMult", "ComplEx", "pRotatE"])
 def test_test_step_query_blocks_reuse_the_table(name):
     """test_step ranks in query blocks of at most 16384 and, from the second
     block (and direction) on, reuses the table statistics and split operands
@@ -257,3 +257,56 @@ def test_protate_three_call_protocol_checks():
         with pytest.raises(RuntimeError, match="list stage"):
             ops.raise_on_device_error(DEV)
     assert total > 0, "the fixture should leave some near-ties for the host"
+
+
+def test_rank_reuse_checks_the_derived_table_kind():
+    """The workspace's derived table is the split-bf16 operands (DistMult /
+    ComplEx) or pRotatE's phase table (k_prot_phase), at the same workspace
+    offset.  A pRotatE call with KGE_RANK_REUSE_TABLE right after a DistMult
+    call on the SAME entity tensor (same pointer and shape) must not take the
+    split for phases (k_rank_tag's kind word), nor a phase table made with
+    another phase divisor (its parameter word): its ranks equal a call on a
+    fresh workspace."""
+    from knowledgegraphembedding_amd import _lib
+    from knowledgegraphembedding_amd.filters import FilterIndex
+    E, R, d = 700, 4, 64
+    md, *_ = build_model("DistMult", E, R, d, 6.0, 11)
+    mp, *_ = build_model("pRotatE", E, R, d, 6.0, 11)
+    mp2, *_ = build_model("pRotatE", E, R, d, 9.0, 11)  # another embedding range: another phase divisor
+    with torch.no_grad():
+        mp.entity_embedding.data = md.entity_embedding.data
+        mp2.entity_embedding.data = md.entity_embedding.data
+    g = np.random.default_rng(12)
+    qs = np.stack([g.integers(0, E, 96), g.integers(0, R, 96), g.integers(0, E, 96)], 1).astype(np.int64)
+    true = np.unique(np.concatenate([qs, np.stack([g.integers(0, E, 800), g.integers(0, R, 800),
+                                                   g.integers(0, E, 800)], 1)]), axis=0)
+    q = torch.from_numpy(qs).to(DEV)
+    off, ids = FilterIndex(true, E, R).filter_csr(qs, "tail-batch")
+    off, ids = torch.from_numpy(off).to(DEV), torch.from_numpy(ids).to(DEV)
+    lib = _lib.load()
+    mode = _lib.MODE_IDS["tail-batch"]
+    nq = qs.shape[0]
+    descs = {"d": md.desc(), "p": mp.desc(), "p2": mp2.desc()}
+    need = max(lib.kge_rank_workspace_bytes(x, nq) for x in descs.values())
+    ws = torch.zeros(need, dtype=torch.uint8, device=DEV)
+    fresh = torch.zeros(need, dtype=torch.uint8, device=DEV)
+    err = ops.state(DEV).err
+    s = ops._stream(DEV)
+
+    def rank(key, buf, flags):
+        r = torch.empty(nq, dtype=torch.int64, device=DEV)
+        t = torch.empty(nq, dtype=torch.int32, device=DEV)
+        _lib.check(lib.kge_rank_filtered_ex(descs[key], mode, q.data_ptr(), nq, off.data_ptr(), ids.data_ptr(),
+                                            r.data_ptr(), t.data_ptr(), None, flags, buf.data_ptr(), buf.numel(),
+                                            err.data_ptr(), s), key)
+        ops.raise_on_device_error(DEV)
+        return r.cpu().numpy(), t.cpu().numpy()
+
+    reuse = ops.RANK_REUSE_TABLE
+    want_p = rank("p", fresh, 0)
+    fresh.zero_()
+    want_p2 = rank("p2", fresh, 0)
+    rank("d", ws, 0)  # the split-bf16 operands land where pRotatE keeps its phases
+    for got, want in ((rank("p", ws, reuse), want_p), (rank("p", ws, reuse), want_p),
+                      (rank("p2", ws, reuse), want_p2), (rank("d", ws, reuse), rank("d", fresh, 0))):
+        assert np.array_equal(got[0], want[0]) and np.array_equal(got[1], want[1])

@@ -1,0 +1,14 @@
+# round 5: pRotatE phase table for the register tile — ranking tests, then
+# the pRotatE evaluation under rocprofv3 (reference and device sin)
+set -o pipefail
+ROOT="${GRAFT_REPO_ROOT:-$(pwd)}"
+O="$ROOT/gpurun_out/r05m"
+mkdir -p "$O"
+cd "$ROOT"
+timeout -k 10 600 python -u -m pytest tests/test_edge_gpu.py tests/test_rank_parity_gpu.py -m gpu -x -v --timeout 300 \
+  --timeout-method thread -p no:cacheprovider --durations=10 > "$O/gpu_tests.log" 2>&1 || exit $?
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/prof" -o run -- \
+  python3 "$ROOT/tools/bench_rank.py" --models pRotatE -d 500 --gamma 6 --reps 3 > "$O/bench_rank_protate.jsonl" 2> "$O/bench_rank.err" || exit $?
+cd "$ROOT"
+timeout -k 10 300 python -u tools/bench_rank.py --models pRotatE -d 500 --gamma 6 --reps 3 --rank-trig device > "$O/bench_rank_protate_device.jsonl" 2>> "$O/bench_rank.err" || exit $?
