@@ -277,10 +277,12 @@ def rank_section(dev, reps: int = 3) -> dict:
 # one reduction element of one (query, candidate) pair — from its inner loop's
 # instruction mix: issue cycles per wave for 64 pair-elements, at
 # 4 SIMDs × 256 CUs × 2.4 GHz (a wave64 VALU instruction, packed or not, 4
-# cycles; v_sqrt 8).  RotatE: v_pk_add (q − e) + v_pk_mul + v_add + v_sqrt +
-# ½ v_pk_add = 22; TransE (round 5): ½ v_pk_add (q − e) + v_add with |·| = 6;
-# pRotatE (round 5): ½ v_pk_mul + ½ v_pk_fma + v_add with |·| = 8.
-TILE_ISSUE_CYC = {"RotatE": 22.0, "TransE": 6.0, "pRotatE": 8.0}
+# cycles; v_sqrt 8).  RotatE (round 5): v_pk_add (q − e: re and im of two
+# candidates, ½ each) + ½ v_pk_mul + ½ v_pk_fma + v_sqrt + ½ v_pk_add = 18
+# (round 4's (re, im)-pair form: 22); TransE (round 5): ½ v_pk_add (q − e) +
+# v_add with |·| = 6; pRotatE (round 5): ½ v_pk_mul + ½ v_pk_fma + v_add with
+# |·| = 8.
+TILE_ISSUE_CYC = {"RotatE": 18.0, "TransE": 6.0, "pRotatE": 8.0}
 
 
 def _rank_timer_read(lib):
