@@ -56,7 +56,15 @@ int check_model(const kge_model_desc* m, Geom* g) {
   const int S = span / g->vec;
   int ns = 1;
   while (64 * ns < S) ns *= 2;
-  if (ns > (g->vec == 4 ? 8 : 32)) return KGE_ERR_DIM;  // (half-)rows up to 2048 floats, any alignment
+  if (ns > (g->vec == 4 ? 8 : 32)) {
+    // (half-)rows over 2048 floats: the run-time-looped kernels of
+    // kge_wide.inc (single-float elements, ns = 0)
+    g->vec = 1;
+    g->ns = 0;
+    g->eg.S = span;
+    g->eg.half = g->cplx ? span : 0;
+    return KGE_OK;
+  }
   g->ns = ns;
   g->eg.S = S;
   g->eg.half = g->cplx ? span : 0;
@@ -280,8 +288,10 @@ int run_grad(const kge_model_desc* m, const Geom& geo, int mode, const int64_t* 
   const int Le = m->entity_dim, Lr = m->relation_dim;
   // k_row's LDS: q (2 padded halves), the merge buffer, the raw scores, the
   // wave states and, with the fused epilogue, the positive's element terms
-  const size_t lds = sizeof(float) * (2 * 64 * (size_t)geo.ns * geo.vec + (size_t)vb_floats(Le) + (size_t)ra.n_lds + 32 +
-                                      (ra.fuse_epi ? 64 * (size_t)geo.ns * geo.vec : 0));
+  const bool wide = (geo.ns == 0);  // rows over 2048 floats (kge_wide.inc)
+  const size_t lds = wide ? wide_row_lds(n)
+                          : sizeof(float) * (2 * 64 * (size_t)geo.ns * geo.vec + (size_t)vb_floats(Le) + (size_t)ra.n_lds +
+                                             32 + (ra.fuse_epi ? 64 * (size_t)geo.ns * geo.vec : 0));
   if (lds > 64 * 1024) return KGE_ERR_DIM;
   const bool all = (phases == KGE_PHASE_ALL);
   if (e_end < 0) e_end = m->nentity;
@@ -297,12 +307,13 @@ int run_grad(const kge_model_desc* m, const Geom& geo, int mode, const int64_t* 
   hipStream_t ss = sd ? sd->s : s;
   int st;
 
-  const int nsl = entity_slices(geo, B, Le);
+  // wide rows: WIDE_PARTS column parts per entity (k_entity_w)
+  const int nsl = wide ? WIDE_PARTS : entity_slices(geo, B, Le);
   const int64_t ent_parts = m->nentity * (int64_t)(nsl > 0 ? nsl : 1);
   // relation pass: as trailing blocks of the sliced entity launch (one call,
   // no stream join); else beside the entity pass on the side stream (always
-  // so in phased calls)
-  const bool rel_fused = all && nsl > 0;
+  // so in phased calls, and for wide rows)
+  const bool rel_fused = all && nsl > 0 && !wide;
   // slice-major q: k_row also writes q as [slice][row][re | im] so each of
   // the entity pass's q reads is 2 KB contiguous and line-aligned (0.240 ->
   // 0.234 ms at the FB15k shape); the single-call step with even slices only
@@ -421,10 +432,10 @@ int run_grad(const kge_model_desc* m, const Geom& geo, int mode, const int64_t* 
   ea.grad_ent = grad_entity;
   ea.write_grad = write_grad;
   ea.nsl = nsl;
-  ea.slice_w = nsl > 0 ? (geo.eg.S + nsl - 1) / nsl : 0;
+  ea.slice_w = nsl > 0 ? (geo.eg.S + nsl - 1) / nsl : 0;  // (wide: elements per part)
   ea.adam = adam_t(adam ? &adam->entity : nullptr);
   ea.adamk = ak;
-  ea.align_sl = q_slm ? 0 : entity_slice_align(nsl, geo.eg.S, Le, m->entity_embedding, write_grad ? grad_entity : nullptr, ea.adam);
+  ea.align_sl = (q_slm || wide) ? 0 : entity_slice_align(nsl, geo.eg.S, Le, m->entity_embedding, write_grad ? grad_entity : nullptr, ea.adam);
   ea.q_sl = q_slm ? w.q_sl : nullptr;
   ea.rel = rl;
   ea.B = B;
@@ -816,7 +827,7 @@ int kge_ship_step(const kge_model_desc* m, int32_t mode, const kge_ship_desc* sh
   ea.grad_ent = grad_entity;
   ea.write_grad = (!adam || adam->write_grad) ? 1 : 0;
   ea.nsl = nsl;
-  ea.slice_w = nsl > 0 ? (geo.eg.S + nsl - 1) / nsl : 0;
+  ea.slice_w = nsl > 0 ? (geo.eg.S + nsl - 1) / nsl : 0;  // (wide: elements per part)
   ea.adam = adam_t(adam ? &adam->entity : nullptr);
   ea.adamk = ak;
   ea.B = B;

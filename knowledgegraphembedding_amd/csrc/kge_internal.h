@@ -84,6 +84,12 @@ struct RowArgs {
 // fused Σw reduction (block_weight_sum) uses as its tree
 __host__ __device__ inline int vb_floats(int Le) { return 2 * Le > 256 ? 2 * Le : 256; }
 
+// Rows wider than the register-tiled kernels hold (kge_wide.inc, check_model's
+// ns = 0): the entity pass cuts each row into WIDE_PARTS column parts (its
+// reg_partial slots per entity), and k_row_w keeps one float per negative in LDS
+constexpr int WIDE_PARTS = 8;
+inline size_t wide_row_lds(int64_t n) { return sizeof(float) * (size_t)(n > 0 ? n : 1); }
+
 struct RelArgs {
   const float* rel;
   int64_t R, E, B, Bn;
@@ -234,6 +240,7 @@ struct RefArgs {
   const float* trig;       // RotatE: [R, 2, Lr] reference cos | sin of the phases, or null
   float fast_u;            // > 0: the fast pass's error bound in u·‖q‖·max‖e‖ (split-bf16 tile)
   int ref_slots;           // k_rank_refine: half-waves with an LDS row slot (set by its launcher)
+  int ref_global;          // k_rank_refine: q and rows read from global memory (rows too wide for LDS)
   // pRotatE with the caller's sin (kge_rank_sin_args / kge_rank_finish_sin):
   // query q's items [item_off[q], item_off[q+1]) — item 0 the true entity, then
   // the listed candidates (or, for an overflowed window, entity ids 0..E-1) —
