@@ -54,7 +54,7 @@ enum kge_status {
     KGE_ERR_SHAPE = 3,      /* entity/relation dims inconsistent with the model (model.py:66-70) */
     KGE_ERR_ARG = 4,        /* null pointer / negative size */
     KGE_ERR_WORKSPACE = 5,  /* workspace smaller than *_workspace_bytes() */
-    KGE_ERR_DIM = 6,        /* row length beyond what the kernels are instantiated for */
+    KGE_ERR_DIM = 6,        /* a size outside a kernel's range (negatives per row, queries per call, LDS) */
     KGE_ERR_ABI = 7,        /* kge_model_desc.struct_size != sizeof(kge_model_desc) of this library */
     KGE_ERR_HIP_BASE = 1000 /* + hipError_t */
 };

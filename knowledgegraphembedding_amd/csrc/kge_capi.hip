@@ -500,7 +500,7 @@ const char* kge_status_string(int status) {
     case KGE_ERR_SHAPE: return "entity/relation dims inconsistent with the model";
     case KGE_ERR_ARG: return "invalid argument";
     case KGE_ERR_WORKSPACE: return "workspace too small";
-    case KGE_ERR_DIM: return "row length / negative count outside the compiled kernel range";
+    case KGE_ERR_DIM: return "size outside the kernels' range (negatives per row, queries per call, LDS; wide rows under query shipping)";
     case KGE_ERR_ABI: return "kge_model_desc.struct_size does not match this library (built against another kge_hip.h)";
     default:
       if (status >= KGE_ERR_HIP_BASE) return hipGetErrorString((hipError_t)(status - KGE_ERR_HIP_BASE));
