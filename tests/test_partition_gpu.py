@@ -177,7 +177,16 @@ def test_row_partition_yago3_10_shape(world, exchange):
     for rank in range(world):
         r = out[rank]
         if exchange == "factors":
-            assert np.array_equal(r["ent"], ent), ("entity rows", rank, float(np.abs(r["ent"] - ent).max()))
+            if not np.array_equal(r["ent"], ent):
+                # which rows (by owner) and columns differ, for the record
+                S = -(-YE // world)
+                badr = np.nonzero((r["ent"] != ent).any(1))[0]
+                owners = np.bincount(SAMPLE_ROWS[badr] // S, minlength=world).tolist()
+                cols = np.nonzero((r["ent"] != ent).any(0))[0]
+                zero = int((r["ent"][badr] == 0).all(1).sum())
+                raise AssertionError(("entity rows", rank, float(np.abs(r["ent"] - ent).max()), "bad rows", len(badr),
+                                      "by owner", owners, "all-zero", zero, "cols", int(cols.min()), int(cols.max()),
+                                      len(cols)))
             assert np.array_equal(r["rel"], rel), ("relation table", rank)
             for got, want in zip(r["logs"], ref):
                 for k in ("positive_sample_loss", "negative_sample_loss", "loss"):
