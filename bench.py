@@ -253,10 +253,10 @@ def rank_section(dev, reps: int = 3) -> dict:
                 best = dt
         flops = 2.0 * 2 * ntest * Ew * K  # fp32 products the ranking needs (both directions)
         # what the matrix cores issue: three bf16 products per fp32 product (hi·hi,
-        # hi·lo, lo·hi; four with KGE_XTILE_LOLO=1) over the tile-padded shape
-        # (128-query and 128-candidate tiles, 16-k slabs)
+        # hi·lo, lo·hi) over the tile-padded shape (128-query and 128-candidate
+        # tiles, 16-k slabs)
         pad = lambda x, m: -(-x // m) * m  # noqa: E731
-        prods = 4 if os.environ.get("KGE_XTILE_LOLO", "0") == "1" else 3
+        prods = 3
         issued = 2.0 * prods * 2 * pad(ntest, 128) * pad(Ew, 128) * pad(K, 16)
         out[name] = {"ms": best * 1e3, "queries_per_s": 2 * ntest / best,
                      "bf16_issued_tflops": issued / best / 1e12, "peak_tflops": 2500.0,
