@@ -485,6 +485,16 @@ int kge_rank_filtered_ex(const kge_model_desc *m, int32_t mode, const int64_t *q
  * list stage's (or after another ranking call used the workspace) sets
  * KGE_DEVERR_ARG.
  */
+/*
+ * Self-test of the bound the pRotatE list stage's interval screen relies on:
+ * writes to max_dist_out (device int32, zeroed by the caller) the largest
+ * distance, in representable floats, between the device's sinf and the
+ * correctly rounded sin over every float x with |x| <= range.  The screen
+ * assumes at most 1 for |x| <= 16 and 2 for |x| <= 65536 (kge_rank_ref.h
+ * SIN_FAST_*); tests/test_rank_parity_gpu.py checks both on each GPU.
+ */
+int kge_selftest_sin(float range, int32_t *max_dist_out, void *stream);
+
 int kge_rank_sin_args(const kge_model_desc *m, int32_t mode, int64_t nq, const int64_t *item_off, float *args_out,
                       void *workspace, size_t workspace_bytes, int32_t *err_flag, void *stream);
 int kge_rank_finish_sin(const kge_model_desc *m, int32_t mode, int64_t nq, const int64_t *item_off,

@@ -145,6 +145,7 @@ SIGNATURES = {
     "kge_rank_sin_args": (C.c_int, [_DESC, _I32, _I64, _P, _P, _P, _SZ, _P, _P]),
     "kge_rank_finish_sin": (C.c_int, [_DESC, _I32, _I64, _P, _P, _P, _P, _P, _P, _SZ, _P, _P]),
     "kge_stage_timer": (C.c_int, [_I32, _P, _I32]),
+    "kge_selftest_sin": (C.c_int, [C.c_float, _P, _P]),
     "kge_sample_negatives": (C.c_int, [_P, _I64, _P, _I64, _I64, _I64, _P, _P, _P, _P, C.c_uint64, _I64, _P, _P, _P,
                                        _P, _P]),
 }

@@ -1220,6 +1220,11 @@ int kge_rank_filtered_ex(const kge_model_desc* m, int32_t mode, const int64_t* q
                    workspace_bytes, err_flag, stream, stage, nullptr, nullptr, nullptr);
 }
 
+int kge_selftest_sin(float range, int32_t* max_dist_out, void* stream) {
+  if (!max_dist_out) return KGE_ERR_ARG;
+  return launch_status(launch_selftest_sin(range, max_dist_out, as_stream(stream)));
+}
+
 int kge_rank_sin_args(const kge_model_desc* m, int32_t mode, int64_t nq, const int64_t* item_off, float* args_out,
                       void* workspace, size_t workspace_bytes, int32_t* err_flag, void* stream) {
   return rank_impl(m, mode, nullptr, nq, nullptr, nullptr, nullptr, nullptr, nullptr, RP_AUTO, workspace,

@@ -41,6 +41,8 @@ int launch_table_stats(const float* ent, int64_t E, int Le, float* stats, hipStr
 // the ranking workspace's table tag (KGE_RANK_REUSE_TABLE; kge_rank_mfma.hip k_rank_tag)
 int launch_rank_tag(int64_t* tag, const float* ent, int64_t E, int Le, int reuse, int need_stats, int split_kind,
                     int64_t split_param, hipStream_t s);
+// kge_selftest_sin (kge_rank_mfma.hip): max float distance of sinf from the correctly rounded sin on |x| ≤ range
+int launch_selftest_sin(float range, int32_t* maxd, hipStream_t s);
 // pRotatE's (cos, sin) / (sin, cos) phase table for the register tile ([rows][K][2]; kge_rank_mfma.hip)
 int launch_prot_phase(const float* src, int64_t rows, int K, float kappa, int ent, float* dst, hipStream_t s,
                       const int64_t* skip = nullptr);

@@ -25,6 +25,7 @@
 #include <cstdlib>
 
 #include "kge_common.h"
+#include "kge_rank_ref.h"
 
 namespace kge {
 
@@ -802,6 +803,28 @@ int launch_prot_phase(const float* src, int64_t rows, int K, float kappa, int en
   if (n == 0) return 0;
   hipLaunchKernelGGL(k_prot_phase, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, src, rows, K, kappa, ent, dst,
                      skip);
+  return (int)hipGetLastError();
+}
+
+// kge_selftest_sin: the largest distance, in floats, between the device sinf
+// and the correctly rounded sin over every float x with |x| ≤ range
+__global__ __launch_bounds__(256) void k_selftest_sin(uint32_t lim, int32_t* maxd) {
+  const uint64_t n = (uint64_t)lim * 2;
+  int32_t m = 0;
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
+    const uint32_t bits = (uint32_t)(i >> 1) | ((i & 1) ? 0x80000000u : 0u);
+    const float x = __int_as_float((int32_t)bits);
+    const int32_t d = float_ord(sin_fast(x)) - float_ord(sin_rn(x));
+    m = max(m, d < 0 ? -d : d);
+  }
+  for (int o = 32; o > 0; o >>= 1) m = max(m, __shfl_xor(m, o));
+  if ((threadIdx.x & 63) == 0 && m > 0) atomicMax(maxd, m);
+}
+
+int launch_selftest_sin(float range, int32_t* maxd, hipStream_t s) {
+  if (!(range >= 0.f) || range > 3.0e38f) return -1;
+  const uint32_t lim = (uint32_t)__builtin_bit_cast(int32_t, range) + 1u;  // bit patterns of [0, range]
+  hipLaunchKernelGGL(k_selftest_sin, dim3(8192), dim3(256), 0, s, lim, maxd);
   return (int)hipGetLastError();
 }
 

@@ -182,19 +182,49 @@ __device__ float ref_score_half(const float* __restrict__ q, const float* __rest
 // pRotatE: the interval the reference's score must lie in when its sin is a
 // library's whose result is within one ulp of the exact value — one of the
 // two floats around sin(x), so within [prev(r), next(r)] of the correctly
-// rounded r (x is the fp32 phase sum; sin(x) is never a float for x ≠ 0).
+// rounded r (x is the fp32 phase sum; sin(x) is never a float for x ≠ 0),
+// bounded here around the device's sinf (see SIN_FAST_*).
 // Every later operation is monotone in its operand — |·| on an interval that
 // does not contain 0, each round-to-nearest add of the sum(dim=2) cascade,
 // the product with the modulus, γ − ·  — so the reference's score lies in
 // [γ − fl(S_hi·mod), γ − fl(S_lo·mod)] (mod ≥ 0; swapped otherwise), S_lo /
 // S_hi the same cascade over the elements' lower / upper |sin| bounds.
 // Returns (lo, hi); NaN in either when an argument is not finite.
+// The device's own fp32 sinf, against the correctly rounded value, checked on
+// every float of the range (kge_selftest_sin; tests/test_rank_parity_gpu.py
+// runs it on each GPU box): at most SIN_FAST_D1 floats apart for |x| ≤
+// SIN_FAST_R1 and SIN_FAST_D2 for |x| ≤ SIN_FAST_R2 (ROCm 7.2: 1 and 2).  So
+// the correctly rounded r lies within that many floats of sinf(x), the
+// library's value within one more, and the interval is taken around sinf(x)
+// — no double-precision sin (the interval screen's cost) — except beyond
+// SIN_FAST_R2, where r is computed as before.
+constexpr float SIN_FAST_R1 = 16.f, SIN_FAST_R2 = 65536.f;
+constexpr int SIN_FAST_D1 = 1, SIN_FAST_D2 = 2;
+__device__ __forceinline__ int32_t float_ord(float f) {  // monotone in f (±0 → 0)
+  const int32_t b = __float_as_int(f);
+  return b >= 0 ? b : -(b & 0x7fffffff);
+}
+__device__ __forceinline__ float ord_float(int32_t o) { return __int_as_float(o >= 0 ? o : ((-o) | (int32_t)0x80000000)); }
+__device__ __forceinline__ float sin_fast(float x) { return sinf(x); }
 __device__ __forceinline__ tf2 abs_sin_bounds(float x) {
-  const float r = sin_rn(x);
-  const float p = nextafterf(r, -INFINITY), n = nextafterf(r, INFINITY);
+  float p, n;
+  const float ax = fabsf(x);
+  if (ax <= SIN_FAST_R2) {
+    const float d = sin_fast(x);
+    const int j = (ax <= SIN_FAST_R1 ? SIN_FAST_D1 : SIN_FAST_D2) + 1;
+    const int32_t o = float_ord(d);
+    p = ord_float(o - j);
+    n = ord_float(o + j);
+  } else {
+    const float r = sin_rn(x);
+    if (r != r) return tf2{r, r};
+    p = nextafterf(r, -INFINITY);
+    n = nextafterf(r, INFINITY);
+  }
+  if (x != x) return tf2{x, x};
   if (p <= 0.f && n >= 0.f) return tf2{0.f, fmaxf(-p, n)};
   const float ap = fabsf(p), an = fabsf(n);
-  return (r != r) ? tf2{r, r} : tf2{fminf(ap, an), fmaxf(ap, an)};
+  return tf2{fminf(ap, an), fmaxf(ap, an)};
 }
 template <int MODE>
 __device__ tf2 ref_score_half_prot_bounds(const float* __restrict__ q, const float* __restrict__ e, int K,

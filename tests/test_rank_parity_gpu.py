@@ -362,3 +362,18 @@ def test_filter_table_matches_query_lists(name, monkeypatch):
     monkeypatch.setenv("KGE_RANK_FILTER_TABLE", "0")
     (rh2, th2), (rt2, tt2) = m.rank_queries_both(test, index)
     assert np.array_equal(rh2, rh) and np.array_equal(rt2, rt) and np.array_equal(th2, th) and np.array_equal(tt2, tt)
+
+
+def test_device_sinf_within_declared_floats():
+    """The pRotatE list stage's interval screen bounds the library's sin around
+    the device's own sinf (kge_rank_ref.h SIN_FAST_*): at most 1 float from the
+    correctly rounded sin for |x| <= 16 and 2 for |x| <= 65536.  Checked here
+    on every float of both ranges, with the library's own compiled sinf
+    (kge_selftest_sin), so a toolchain whose sinf drifts fails this test
+    instead of producing wrong ranks."""
+    from knowledgegraphembedding_amd import _lib, ops
+    lib = _lib.load()
+    for rng, bound in ((16.0, 1), (65536.0, 2)):
+        out = torch.zeros(1, dtype=torch.int32, device=DEV)
+        _lib.check(lib.kge_selftest_sin(rng, out.data_ptr(), ops._stream(DEV)), "kge_selftest_sin")
+        assert int(out.item()) <= bound, (rng, int(out.item()))
