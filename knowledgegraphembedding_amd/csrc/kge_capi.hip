@@ -1131,10 +1131,11 @@ int rank_impl(const kge_model_desc* m, int32_t mode, const int64_t* queries, int
       if (!st) st = launch_status(launch_prot_phase(m->entity_embedding, m->nentity, K, kappa, 1, w.eph, s, w.tag + 6));
       if (st) return st;
     }
-    // split-bf16 path: s_true in the reference's order after the window
-    // (k_rank_true_ref, rows of ≤ 1024 floats: its LDS); wider rows take the
-    // tile's own gather mode here (the window then covers two fast scores)
-    const bool true_ref = rp == RP_MFMA && ((m->entity_dim + 3) & ~3) <= 1024;
+    // s_true in the reference's order after the window (k_rank_true_ref):
+    // the split-bf16 path (instead of its gather pass) and RotatE on the
+    // register tile (after its gather pass, whose fast s_true sizes the
+    // window's S); the window then covers the candidate's error only
+    const bool true_ref = rp == RP_MFMA || (rp == RP_TILE && m->model == KGE_ROTATE);
     if (rp == RP_MFMA) {
       st = launch_status(launch_split_bf16(w.q, nq, m->entity_dim, w.qs, s));
       if (!st)
