@@ -30,67 +30,74 @@ from .model import KGEModel
 from .optim import KGEAdam
 
 
+_FLAG = dict(action='store_true')
+
+# The reference's command line (codes/run.py:24-72): the same flags, short
+# forms, defaults and types, plus two extensions at the end.
+_CLI = (
+    (('--cuda',), dict(_FLAG, help='compute on the GPU (implied: there is no CPU path)')),
+    (('--do_train',), _FLAG),
+    (('--do_valid',), _FLAG),
+    (('--do_test',), _FLAG),
+    (('--evaluate_train',), dict(_FLAG, help='also rank the training triples')),
+    (('--countries',), dict(_FLAG, help='Countries S1/S2/S3: AUC-PR over the regions')),
+    (('--regions',), dict(type=int, nargs='+', default=None, help='filled in from regions.list, not by hand')),
+    (('--data_path',), dict(type=str, default=None)),
+    (('--model',), dict(default='TransE', type=str)),
+    (('-de', '--double_entity_embedding'), _FLAG),
+    (('-dr', '--double_relation_embedding'), _FLAG),
+    (('-n', '--negative_sample_size'), dict(default=128, type=int)),
+    (('-d', '--hidden_dim'), dict(default=500, type=int)),
+    (('-g', '--gamma'), dict(default=12.0, type=float)),
+    (('-adv', '--negative_adversarial_sampling'), _FLAG),
+    (('-a', '--adversarial_temperature'), dict(default=1.0, type=float)),
+    (('-b', '--batch_size'), dict(default=1024, type=int)),
+    (('-r', '--regularization'), dict(default=0.0, type=float)),
+    (('--test_batch_size',), dict(default=4, type=int, help='queries per ranking batch')),
+    (('--uni_weight',), dict(_FLAG, help='plain means instead of the word2vec-style subsampling weights')),
+    (('-lr', '--learning_rate'), dict(default=0.0001, type=float)),
+    (('-cpu', '--cpu_num'), dict(default=10, type=int)),
+    (('-init', '--init_checkpoint'), dict(default=None, type=str)),
+    (('-save', '--save_path'), dict(default=None, type=str)),
+    (('--max_steps',), dict(default=100000, type=int)),
+    (('--warm_up_steps',), dict(default=None, type=int)),
+    (('--save_checkpoint_steps',), dict(default=10000, type=int)),
+    (('--valid_steps',), dict(default=10000, type=int)),
+    (('--log_steps',), dict(default=100, type=int, help='training log interval in steps')),
+    (('--test_log_steps',), dict(default=1000, type=int, help='evaluation log interval in batches')),
+    (('--nentity',), dict(type=int, default=0, help='filled in from entities.dict, not by hand')),
+    (('--nrelation',), dict(type=int, default=0, help='filled in from relations.dict, not by hand')),
+    (('--row_partition',), dict(_FLAG, help='multi-GPU only: each rank owns 1/world of the entity rows and '
+                                            'their Adam state (partition.py; KGE_PART_EXCHANGE=factors|grads|'
+                                            'queries, "queries" keeps only the shard on each rank and ships q '
+                                            'vectors instead of rows)')),
+    (('--device_sampler',), dict(_FLAG, help='build training batches on the GPU (sampler.py) instead of the '
+                                             'CPU TrainDataset workers: same sampling semantics, a different '
+                                             'random stream')),
+)
+
+# what -init restores from the checkpoint's config.json (codes/run.py:75-90);
+# data_path only when the command line gives none
+_RESTORED = ('countries', 'model', 'double_entity_embedding', 'double_relation_embedding', 'hidden_dim',
+             'test_batch_size')
+
+
 def parse_args(args=None):
-    parser = argparse.ArgumentParser(
-        description='Training and Testing Knowledge Graph Embedding Models',
-        usage='train.py [<args>] [-h | --help]'
-    )
-    parser.add_argument('--cuda', action='store_true', help='use GPU')
-    parser.add_argument('--do_train', action='store_true')
-    parser.add_argument('--do_valid', action='store_true')
-    parser.add_argument('--do_test', action='store_true')
-    parser.add_argument('--evaluate_train', action='store_true', help='Evaluate on training data')
-    parser.add_argument('--countries', action='store_true', help='Use Countries S1/S2/S3 datasets')
-    parser.add_argument('--regions', type=int, nargs='+', default=None,
-                        help='Region Id for Countries S1/S2/S3 datasets, DO NOT MANUALLY SET')
-    parser.add_argument('--data_path', type=str, default=None)
-    parser.add_argument('--model', default='TransE', type=str)
-    parser.add_argument('-de', '--double_entity_embedding', action='store_true')
-    parser.add_argument('-dr', '--double_relation_embedding', action='store_true')
-    parser.add_argument('-n', '--negative_sample_size', default=128, type=int)
-    parser.add_argument('-d', '--hidden_dim', default=500, type=int)
-    parser.add_argument('-g', '--gamma', default=12.0, type=float)
-    parser.add_argument('-adv', '--negative_adversarial_sampling', action='store_true')
-    parser.add_argument('-a', '--adversarial_temperature', default=1.0, type=float)
-    parser.add_argument('-b', '--batch_size', default=1024, type=int)
-    parser.add_argument('-r', '--regularization', default=0.0, type=float)
-    parser.add_argument('--test_batch_size', default=4, type=int, help='valid/test batch size')
-    parser.add_argument('--uni_weight', action='store_true',
-                        help='Otherwise use subsampling weighting like in word2vec')
-    parser.add_argument('-lr', '--learning_rate', default=0.0001, type=float)
-    parser.add_argument('-cpu', '--cpu_num', default=10, type=int)
-    parser.add_argument('-init', '--init_checkpoint', default=None, type=str)
-    parser.add_argument('-save', '--save_path', default=None, type=str)
-    parser.add_argument('--max_steps', default=100000, type=int)
-    parser.add_argument('--warm_up_steps', default=None, type=int)
-    parser.add_argument('--save_checkpoint_steps', default=10000, type=int)
-    parser.add_argument('--valid_steps', default=10000, type=int)
-    parser.add_argument('--log_steps', default=100, type=int, help='train log every xx steps')
-    parser.add_argument('--test_log_steps', default=1000, type=int, help='valid/test log every xx steps')
-    parser.add_argument('--nentity', type=int, default=0, help='DO NOT MANUALLY SET')
-    parser.add_argument('--nrelation', type=int, default=0, help='DO NOT MANUALLY SET')
-    parser.add_argument('--row_partition', action='store_true',
-                        help='multi-GPU only: each rank owns 1/world of the entity rows and their Adam state '
-                             '(partition.py; KGE_PART_EXCHANGE=factors|grads|queries, "queries" keeps only '
-                             'the shard on each rank and ships q vectors instead of rows)')
-    parser.add_argument('--device_sampler', action='store_true',
-                        help='build training batches on the GPU (sampler.py) instead of the CPU TrainDataset '
-                             'workers: same sampling semantics, a different random stream')
-    return parser.parse_args(args)
+    cli = argparse.ArgumentParser(description='Training and Testing Knowledge Graph Embedding Models',
+                                  usage='train.py [<args>] [-h | --help]')
+    for names, options in _CLI:
+        cli.add_argument(*names, **options)
+    return cli.parse_args(args)
 
 
 def override_config(args):
     '''Restore the model/data configuration of -init (run.py:75-90).'''
-    with open(os.path.join(args.init_checkpoint, 'config.json'), 'r') as fjson:
-        argparse_dict = json.load(fjson)
-    args.countries = argparse_dict['countries']
+    with open(os.path.join(args.init_checkpoint, 'config.json')) as f:
+        saved = json.load(f)
+    for key in _RESTORED:
+        setattr(args, key, saved[key])
     if args.data_path is None:
-        args.data_path = argparse_dict['data_path']
-    args.model = argparse_dict['model']
-    args.double_entity_embedding = argparse_dict['double_entity_embedding']
-    args.double_relation_embedding = argparse_dict['double_relation_embedding']
-    args.hidden_dim = argparse_dict['hidden_dim']
-    args.test_batch_size = argparse_dict['test_batch_size']
+        args.data_path = saved['data_path']
 
 
 def _json_args(args):
@@ -113,23 +120,19 @@ def save_model(model, optimizer, save_variable_list, args, optimizer_state=None)
     np.save(os.path.join(args.save_path, 'relation_embedding'), model.relation_embedding.detach().cpu().numpy())
 
 
+def _tsv(file_path):
+    with open(file_path) as f:
+        return [line.strip().split('\t') for line in f]
+
+
 def read_triple(file_path, entity2id, relation2id):
     '''Triples mapped to ids (run.py:123-132).'''
-    triples = []
-    with open(file_path) as fin:
-        for line in fin:
-            h, r, t = line.strip().split('\t')
-            triples.append((entity2id[h], relation2id[r], entity2id[t]))
-    return triples
+    return [(entity2id[h], relation2id[r], entity2id[t]) for h, r, t in _tsv(file_path)]
 
 
 def read_dict(file_path):
-    out = dict()
-    with open(file_path) as fin:
-        for line in fin:
-            eid, name = line.strip().split('\t')
-            out[name] = int(eid)
-    return out
+    '''name → id of entities.dict / relations.dict (lines "<id>\\t<name>").'''
+    return {name: int(eid) for eid, name in _tsv(file_path)}
 
 
 def shared_seed(group=None) -> int:
@@ -269,28 +272,21 @@ def main(args):
         logging.info('--cuda implied: knowledgegraphembedding_amd has no CPU compute path')
         args.cuda = True
 
-    entity2id = read_dict(os.path.join(args.data_path, 'entities.dict'))
-    relation2id = read_dict(os.path.join(args.data_path, 'relations.dict'))
+    entity2id, relation2id = (read_dict(os.path.join(args.data_path, f + '.dict')) for f in ('entities', 'relations'))
     if args.countries:
-        regions = list()
-        with open(os.path.join(args.data_path, 'regions.list')) as fin:
-            for line in fin:
-                regions.append(entity2id[line.strip()])
-        args.regions = regions
+        with open(os.path.join(args.data_path, 'regions.list')) as f:
+            args.regions = [entity2id[name.strip()] for name in f]
 
     nentity, nrelation = len(entity2id), len(relation2id)
     args.nentity, args.nrelation = nentity, nrelation
-    logging.info('Model: %s' % args.model)
-    logging.info('Data Path: %s' % args.data_path)
-    logging.info('#entity: %d' % nentity)
-    logging.info('#relation: %d' % nrelation)
-
-    train_triples = read_triple(os.path.join(args.data_path, 'train.txt'), entity2id, relation2id)
-    logging.info('#train: %d' % len(train_triples))
-    valid_triples = read_triple(os.path.join(args.data_path, 'valid.txt'), entity2id, relation2id)
-    logging.info('#valid: %d' % len(valid_triples))
-    test_triples = read_triple(os.path.join(args.data_path, 'test.txt'), entity2id, relation2id)
-    logging.info('#test: %d' % len(test_triples))
+    for line in ('Model: %s' % args.model, 'Data Path: %s' % args.data_path, '#entity: %d' % nentity,
+                 '#relation: %d' % nrelation):
+        logging.info(line)
+    split = {}
+    for name in ('train', 'valid', 'test'):
+        split[name] = read_triple(os.path.join(args.data_path, name + '.txt'), entity2id, relation2id)
+        logging.info('#%s: %d' % (name, len(split[name])))
+    train_triples, valid_triples, test_triples = split['train'], split['valid'], split['test']
     all_true_triples = train_triples + valid_triples + test_triples
 
     kge_model = KGEModel(model_name=args.model, nentity=nentity, nrelation=nrelation, hidden_dim=args.hidden_dim,
@@ -373,15 +369,15 @@ def main(args):
         init_step = 0
 
     step = init_step
-    logging.info('Start Training...')
-    logging.info('init_step = %d' % init_step)
-    logging.info('batch_size = %d' % args.batch_size)
-    logging.info('negative_adversarial_sampling = %d' % args.negative_adversarial_sampling)
-    logging.info('hidden_dim = %d' % args.hidden_dim)
-    logging.info('gamma = %f' % args.gamma)
-    logging.info('negative_adversarial_sampling = %s' % str(args.negative_adversarial_sampling))
+    # the reference's start-up lines, verbatim (negative_adversarial_sampling twice, as %d and as %s)
+    lines = ['Start Training...', 'init_step = %d' % init_step, 'batch_size = %d' % args.batch_size,
+             'negative_adversarial_sampling = %d' % args.negative_adversarial_sampling,
+             'hidden_dim = %d' % args.hidden_dim, 'gamma = %f' % args.gamma,
+             'negative_adversarial_sampling = %s' % str(args.negative_adversarial_sampling)]
     if args.negative_adversarial_sampling:
-        logging.info('adversarial_temperature = %f' % args.adversarial_temperature)
+        lines.append('adversarial_temperature = %f' % args.adversarial_temperature)
+    for line in lines:
+        logging.info(line)
 
     if args.do_train:
         logging.info('learning_rate = %d' % current_learning_rate)
@@ -424,18 +420,13 @@ def main(args):
 
     if rank != 0:
         return
-    if args.do_valid:
-        logging.info('Evaluating on Valid Dataset...')
-        metrics = kge_model.test_step(kge_model, valid_triples, all_true_triples, args)
-        log_metrics('Valid', step, metrics)
-    if args.do_test:
-        logging.info('Evaluating on Test Dataset...')
-        metrics = kge_model.test_step(kge_model, test_triples, all_true_triples, args)
-        log_metrics('Test', step, metrics)
-    if args.evaluate_train:
-        logging.info('Evaluating on Training Dataset...')
-        metrics = kge_model.test_step(kge_model, train_triples, all_true_triples, args)
-        log_metrics('Test', step, metrics)
+    # final evaluations (the training split is logged under 'Test', as in the reference)
+    for wanted, title, triples, label in ((args.do_valid, 'Valid', valid_triples, 'Valid'),
+                                          (args.do_test, 'Test', test_triples, 'Test'),
+                                          (args.evaluate_train, 'Training', train_triples, 'Test')):
+        if wanted:
+            logging.info('Evaluating on %s Dataset...' % title)
+            log_metrics(label, step, kge_model.test_step(kge_model, triples, all_true_triples, args))
 
 
 if __name__ == '__main__':
