@@ -1132,10 +1132,12 @@ int rank_impl(const kge_model_desc* m, int32_t mode, const int64_t* queries, int
       if (st) return st;
     }
     // s_true in the reference's order after the window (k_rank_true_ref):
-    // the split-bf16 path (instead of its gather pass) and RotatE on the
-    // register tile (after its gather pass, whose fast s_true sizes the
-    // window's S); the window then covers the candidate's error only
-    const bool true_ref = rp == RP_MFMA || (rp == RP_TILE && m->model == KGE_ROTATE);
+    // the split-bf16 path (instead of its gather pass), RotatE and pRotatE on
+    // the register tile (after its gather pass, whose fast s_true sizes the
+    // window's S; pRotatE: a point of the reference score's interval, the
+    // window widened by its width); the window then covers the candidate's
+    // error only
+    const bool true_ref = rp == RP_MFMA || (rp == RP_TILE && (m->model == KGE_ROTATE || prot_tile));
     if (rp == RP_MFMA) {
       st = launch_status(launch_split_bf16(w.q, nq, m->entity_dim, w.qs, s));
       if (!st)
