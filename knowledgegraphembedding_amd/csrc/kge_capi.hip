@@ -87,7 +87,9 @@ int rank_path(const kge_model_desc* m, int requested) {
   const bool x_ok = bil && (uint64_t)xsplit_elems(m->nentity, m->entity_dim) * 2u < 0x7FFFFFF0ull;
   const bool mfma_ok = bil && (m->entity_dim % 4 == 0) && al &&
                        (uint64_t)m->nentity * (uint64_t)m->entity_dim * 4u < 0xFFFFFF00ull;
-  const bool tile_ok = (K % 4 == 0) && al;
+  // (the register tile's counting pass reads a block's 64 rows — pRotatE:
+  // their 2K-float phase rows — through one buffer descriptor)
+  const bool tile_ok = (K % 4 == 0) && al && (uint64_t)64 * 2 * (uint64_t)m->entity_dim * 4u < 0x7FFFFFF0ull;
   if (requested == RP_MFMA) return x_ok ? RP_MFMA : -1;
   if (requested == RP_MFMA32) return mfma_ok ? RP_MFMA32 : -1;
   if (requested == RP_TILE) return tile_ok ? RP_TILE : -1;
