@@ -475,10 +475,19 @@ def main():
     import ctypes
     _lib.check(lib.kge_stage_timer(2, stage.ctypes.data_as(ctypes.c_void_p), 7), "kge_stage_timer")
     lib.kge_stage_timer(0, None, 0)
+    replica_check = None
     if group is not None:
         t = torch.tensor([dt], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
+        # after the timed steps (outside the clock): every exchange that keeps a
+        # replicated table must leave it bit-identical on every rank
+        from knowledgegraphembedding_amd.distributed import replicas_disagree, table_fingerprint
+        fp = part.replica_checksums() if part is not None else \
+            table_fingerprint(model.entity_embedding, model.relation_embedding)
+        bad = replicas_disagree(fp, group)
+        replica_check = {"tables": "relation only (query shipping keeps no replica)" if fp.numel() == 1 else
+                         "entity replica + relation", "ranks_differing_from_rank0": bad, "agree": not bad}
 
     calls = max(1.0, float(stage[6]))
     here = os.path.dirname(os.path.abspath(__file__))
@@ -530,6 +539,7 @@ def main():
     if group is not None:
         dist_info["backend"] = str(dist.get_backend(group))
         dist_info["world_size"] = dist.get_world_size(group)
+        dist_info["replica_check"] = replica_check
     try:
         dist_info["rccl_version"] = ".".join(str(x) for x in torch.cuda.nccl.version())
     except Exception:  # noqa: BLE001 — reported as unknown, never fatal

@@ -124,7 +124,7 @@ struct Carver {
 struct GradWs {
   float *g, *q, *dq, *ent_contrib, *rel_contrib, *row_stats, *reg_partial, *wsum;
   int32_t *keys, *cnt, *off, *tmp, *occ;
-  float* q_sl;  // slice-major q for the sliced entity pass (KGE_ENT_QSL)
+  float* q_sl;  // slice-major q for the sliced entity pass (single-call steps with even slices)
   void* scan_tmp;
   size_t scan_tmp_bytes;
 };
@@ -248,7 +248,7 @@ int entity_slices(const Geom& geo, int64_t B, int Le) {
 // line boundaries of the row's first half.  Only when every stream of the pass
 // (table = Adam param, gradient, moments) has the same phase, every row's
 // phase is one the 64-slot slices absorb (last slice ≤ 64 slots) — d = 1000:
-// phases 0 and 4 — and KGE_ENT_ALIGN is not 0.
+// phases 0 and 4.
 int entity_slice_align(int nsl, int S, int Le, const float* ent, const float* grad, const AdamT& ad) {
   if (nsl < 2) return 0;
   const uintptr_t base = (uintptr_t)ent & 127;

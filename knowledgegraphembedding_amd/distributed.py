@@ -281,6 +281,26 @@ def dp_train_step_factors(model, positive_sample, negative_sample, subsampling_w
     return losses
 
 
+def table_fingerprint(*tables) -> torch.Tensor:
+    """[len(tables)] int64: each fp32 table's bit patterns summed as integers
+    (any changed bit of any element changes it, bar exact cancellations)."""
+    return torch.stack([torch.sum(t.detach().reshape(-1).view(torch.int32), dtype=torch.int64) for t in tables])
+
+
+def replicas_disagree(fingerprint: torch.Tensor, group=None) -> list:
+    """Collective: the ranks whose replica fingerprint differs from rank 0's
+    (empty when every rank holds the same bits).  The exchanges that keep a
+    replicated table — factors, owner-computes, the row partition's
+    reduce-scatter — leave it bit-identical on every rank after each step;
+    bench.py checks that after its timed steps at N > 1, so a replica that
+    diverged on one rank shows in the driver's line instead of staying silent."""
+    world = dist.get_world_size(group)
+    allfp = torch.empty(world * fingerprint.numel(), dtype=fingerprint.dtype, device=fingerprint.device)
+    dist.all_gather_into_tensor(allfp, fingerprint.contiguous(), group=group)
+    allfp = allfp.view(world, -1).cpu()
+    return [r for r in range(world) if not torch.equal(allfp[r], allfp[0])]
+
+
 def dp_weight_sum(subsampling_weight: torch.Tensor, group=None) -> torch.Tensor:
     ws = subsampling_weight.float().sum().reshape(1)
     dist.all_reduce(ws, op=dist.ReduceOp.SUM, group=group)

@@ -169,8 +169,7 @@ class EntityRowPartition:
             return
         if self._pending:
             for work, stage, c0, c1 in self._pending:
-                work.wait()
-                self._gloo_device_sync()
+                work.wait()  # the caller's stream now waits for the gather's output (RCCL and gloo alike)
                 # stage row r·(c1-c0) + j = rank r's shard row c0 + j
                 self.full.view(self.world, self.rows, self.dim)[:, c0:c1].copy_(
                     stage.view(self.world, c1 - c0, self.dim))
@@ -394,21 +393,22 @@ class EntityRowPartition:
         places them at replica rows r·S + c0 ….  One staging buffer per chunk,
         so the gathers of consecutive chunks can be on the wire together."""
         stage = self._stage_buf(c0, c1 - c0, self.full.device)
-        self._gloo_device_sync()
+        # the collective's input is ordered after the chunk's entity pass (the
+        # caller's stream at issue); its output after gather()'s copy of the
+        # previous step (DESIGN §9, "the owner step's hand-offs")
         work = dist.all_gather_into_tensor(stage, self.full[self.lo + c0:self.lo + c1], group=self.group,
                                            async_op=True)
         self._pending.append((work, stage, c0, c1))
 
-    def _gloo_device_sync(self) -> None:
-        """gloo (the multi-rank GPU tests: ranks sharing one card) moves CUDA
-        tensors through pinned host copies on streams of its own; around the
-        owner step's async row gathers the device is synchronised as well, so
-        their order does not rest on those streams' events alone (one run of
-        the world-8 owner test in round 5 found some rank-3 replica rows zero
-        — all or a leading part of a row — and the next run passed; RCCL
-        orders its stream itself and skips this)."""
-        if self.full.is_cuda and dist.get_backend(self.group) == "gloo":
-            torch.cuda.synchronize(self.full.device)
+    def replica_checksums(self) -> torch.Tensor:
+        """This rank's [2] int64 fingerprint of its replica (the bit patterns of
+        the entity rows, then of the relation table, summed as integers): equal
+        on every rank exactly when the replicas agree bit for bit, as the
+        owner-computes and reduce-scatter exchanges guarantee.  Query
+        shipping keeps no replica: [1], the relation table alone."""
+        if self.full is None:
+            return _dist.table_fingerprint(self.model.relation_embedding)
+        return _dist.table_fingerprint(self.full, self.model.relation_embedding)
 
     def _owner_chunks(self):
         """Shard row ranges [c0, c1) of the chunked owner step (OWNER_CHUNKS

@@ -229,3 +229,31 @@ def test_rank_shards_disjoint_with_per_rank_torch_seeds(world):
         union = set().union(*map(set, shards))
         assert len(union) == world * (103 // world)
     assert out[0][1] != out[0][2]
+
+
+def _fp_worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.manual_seed(5)
+    ent, rel = torch.randn(37, 6), torch.randn(4, 3)
+    same = kdist.replicas_disagree(kdist.table_fingerprint(ent, rel))
+    if rank == 2:  # one rank's replica diverges: one row zeroed, then one bit of the relation table
+        ent[11, :2] = 0.0
+    after_row = kdist.replicas_disagree(kdist.table_fingerprint(ent, rel))
+    if rank == 2:
+        ent[11, :2] = torch.randn(37, 6, generator=torch.Generator().manual_seed(5))[11, :2]
+        rel.view(-1).view(torch.int32)[5] ^= 1
+    after_bit = kdist.replicas_disagree(kdist.table_fingerprint(ent, rel))
+    out[rank] = (same, after_row, after_bit)
+    dist.destroy_process_group()
+
+
+def test_replica_fingerprint_names_diverged_rank():
+    """bench.py's multi-GPU replica check (distributed.replicas_disagree):
+    identical replicas agree; a leading part of one rank's row zeroed, or one
+    flipped bit of its relation table, names exactly that rank on every rank."""
+    world = 3
+    out = mp.Manager().dict()
+    mp.spawn(_fp_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    for r in range(world):
+        assert out[r] == ([], [2], [2]), (r, out[r])

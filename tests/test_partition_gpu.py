@@ -119,11 +119,14 @@ def _yago_worker(rank, world, port, exchange, out):
     opt = KGEAdam(part.parameters(), lr=1e-4)
     sl = slice(rank * YB, (rank + 1) * YB)
     it = iter([(p[sl], n[sl], w[sl], m) for p, n, w, m in _yago_batches("cuda:0", world)])
-    logs = [dict(KGEModel.train_step(model, opt, it, _args(dist.group.WORLD))) for _ in range(2)]
+    logs, fps = [], []
+    for _ in range(2):
+        logs.append(dict(KGEModel.train_step(model, opt, it, _args(dist.group.WORLD))))
+        fps.append(part.replica_checksums().cpu().numpy())  # per step: which step a replica diverged in
     torch.cuda.synchronize()
     ent = part.materialize()  # query shipping: the shards gathered (collective); otherwise the replica
     res = {"logs": logs, "ent": ent.detach()[torch.from_numpy(SAMPLE_ROWS).cuda()].cpu().numpy(),
-           "rel": model.relation_embedding.detach().cpu().numpy()}
+           "rel": model.relation_embedding.detach().cpu().numpy(), "fps": fps}
     if rank == 0:
         # 8 rows' scores of the trained (gathered) table against the oracle's op chain on the same table
         from oracle import kge_oracle as O
@@ -174,6 +177,11 @@ def test_row_partition_yago3_10_shape(world, exchange):
         assert bad.sum() <= max(2, 1e-5 * got.size), (what, int(bad.sum()))
         assert np.abs(got - want).max() <= 2 * 2 * 1e-4 + 1e-6, what
 
+    # every rank's replica (query shipping: relation table) fingerprint, per step, equals rank 0's
+    fps = [out[r]["fps"] for r in range(world)]
+    for step in range(2):
+        diverged = [r for r in range(world) if not np.array_equal(fps[r][step], fps[0][step])]
+        assert not diverged, ("replica fingerprints differ from rank 0's after step", step + 1, diverged)
     for rank in range(world):
         r = out[rank]
         if exchange == "factors":
