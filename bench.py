@@ -375,6 +375,58 @@ def distance_rank_section(dev, reps: int = 3) -> dict:
     return out
 
 
+def test_step_section(dev) -> dict:
+    """What run.sh's --do_test waits on (run.py → KGEModel.test_step,
+    model.py:346-429): filtered MRR / MR / HITS over a whole FB15k-size test
+    split, end to end — the reference's list-of-tuples inputs, FilterIndex
+    construction over train + valid + test, query blocks, both directions,
+    reference-order refinement and the metric aggregation.  RotatE FB15k
+    (E = 14951, R = 1345, d = 1000 -de, γ = 24, best_config.sh:3), synthetic
+    483,142 train + 50,000 valid + 59,071 test triples (all_true = their
+    union), 118,142 queries.  `host_s` = the wall time not covered by the
+    ranking calls' device spans (kge_stage_timer 4/5: call start → ranks
+    written), i.e. index build, per-block filter CSRs, launches, read-back and
+    the metric sums."""
+    import numpy as np
+    from knowledgegraphembedding_amd import synth
+    from knowledgegraphembedding_amd.filters import FilterIndex
+    Ef, Rf = 14951, 1345
+
+    def trip(seed, n):
+        return np.stack([synth.randint(seed, (n,), Ef), synth.randint(seed + 1, (n,), Rf),
+                         synth.randint(seed + 2, (n,), Ef)], 1).astype(np.int64)
+
+    train, valid, test = trip(11, 483142), trip(21, 50000), trip(31, 59071)
+    all_true = [tuple(x) for x in np.concatenate([train, valid, test]).tolist()]  # run.py's read_triple lists
+    test_l = [tuple(x) for x in test.tolist()]
+    torch.manual_seed(0)
+    m = KGEModel("RotatE", Ef, Rf, 1000, 24.0, True, False).to(dev)
+    args = Namespace(countries=False, nentity=Ef, nrelation=Rf, test_batch_size=16, cpu_num=10,
+                     test_log_steps=10 ** 9, cuda=True)
+    KGEModel.test_step(m, test_l[:64], all_true[:4096], args)  # warm-up: first-use state, not timed
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    FilterIndex(all_true, Ef, Rf)
+    t_index = time.perf_counter() - t0
+    lib = _lib.load()
+    _lib.check(lib.kge_stage_timer(4, None, 0), "kge_stage_timer")
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    met = KGEModel.test_step(m, test_l, all_true, args)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    st = _rank_timer_read(lib)
+    lib.kge_stage_timer(0, None, 0)
+    dev_s = float(st[0] + st[1] + st[2]) * 1e-3
+    del m
+    torch.cuda.empty_cache()
+    return {"workload": "KGEModel.test_step, RotatE FB15k E=14951 R=1345 d=1000 -de, 59,071 test triples "
+                        "(118,142 filtered queries), synthetic 592,213-triple filter graph, list-of-tuples inputs",
+            "seconds": dt, "queries_per_s": 2 * len(test_l) / dt, "filter_index_build_s": t_index,
+            "ranking_device_s": dev_s, "host_s": max(0.0, dt - dev_s), "host_share": max(0.0, dt - dev_s) / dt,
+            "directions_timed": int(st[3]), "MRR": met["MRR"]}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -596,6 +648,7 @@ def main():
         print(f"bench.py: a roofline fraction exceeds 1 ({fr}); the byte model is wrong", file=sys.stderr)
     if rank == 0 and world == 1 and not a.no_rank and a.workload == "fb15k":
         out["ranking"] = rank_section(dev)
+        out["test_step"] = test_step_section(dev)
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         # the full batch at config 2's n = 256; config 5's n = 1024 at a quarter of the rows (one full
         # step there would hold ~40 GB of temporaries and take minutes)

@@ -100,9 +100,10 @@ typedef struct kge_model_desc {
 
 /* Library identity: "knowledgegraphembedding_amd <KGE_ABI_VERSION> gfx950".  The
  * version changes with every change of a struct, a signature or a call
- * protocol in this header (0.3: pRotatE's three-call item counts);
+ * protocol in this header (0.3: pRotatE's three-call item counts; 0.4:
+ * kge_rank_filtered_both, the ranking timer counting directions);
  * loaders refuse a library whose version differs from the header they bind. */
-#define KGE_ABI_VERSION "0.3"
+#define KGE_ABI_VERSION "0.4"
 const char *kge_version(void);
 const char *kge_status_string(int status);
 
@@ -451,6 +452,28 @@ int kge_rank_filtered_ex(const kge_model_desc *m, int32_t mode, const int64_t *q
                          const int64_t *filt_off, const int64_t *filt_ids, int64_t *ranks_out,
                          int32_t *ties_out, int32_t *listed_out, int32_t path, void *workspace,
                          size_t workspace_bytes, int32_t *err_flag, void *stream);
+/*
+ * Both directions of one evaluation in one pass (model.py:349-418 ranks every
+ * test triple as a head-batch query, then as a tail-batch query): the same
+ * ranks and ties as kge_rank_filtered_ex(KGE_HEAD_BATCH, ...) followed by
+ * kge_rank_filtered_ex(KGE_TAIL_BATCH, ...) on the same queries, written to
+ *   ranks_out / ties_out / listed_out [2·nq]: the head-batch direction's nq,
+ *   then the tail-batch direction's;
+ * filt_off_head / filt_ids_head and filt_off_tail / filt_ids_tail: each
+ * direction's filter (per-query lists, or with KGE_RANK_FILTER_TABLE each
+ * direction's whole filter index).  The workspace holds 2·nq queries
+ * (kge_rank_workspace_bytes(m, 2·nq)).  The mode-independent stages — the
+ * table's statistics and split operands, the split of every q, the MFMA
+ * counting tile and the emission — run once over all 2·nq queries; the
+ * mode-dependent ones (q, filter bitmap, windows, refinement) once per
+ * direction.  Not with KGE_RANK_STAGE_LIST (pRotatE's three-call form is per
+ * direction): KGE_ERR_ARG.
+ */
+int kge_rank_filtered_both(const kge_model_desc *m, const int64_t *queries, int64_t nq,
+                           const int64_t *filt_off_head, const int64_t *filt_ids_head,
+                           const int64_t *filt_off_tail, const int64_t *filt_ids_tail, int64_t *ranks_out,
+                           int32_t *ties_out, int32_t *listed_out, int32_t path, void *workspace,
+                           size_t workspace_bytes, int32_t *err_flag, void *stream);
 
 /*
  * pRotatE ranks bit-exact to the reference — whose sin (model.py:245) is its
@@ -522,14 +545,16 @@ int kge_rank_finish_sin(const kge_model_desc *m, int32_t mode, int64_t nq, const
  *   command 4: enable and reset the RANKING timer: every kge_rank_filtered* call
  *              (and pRotatE's three-call form, list → finish) records events
  *              at its start, around its fast counting pass and after its ranks
- *              are written (command 0 disables it too);
+ *              are written (every finish call of the three-call form marks
+ *              "ranks written"; the last one before the next call counts)
+ *              (command 0 disables it too);
  *   command 5: synchronise them and write the summed milliseconds of its
  *              KGE_RANK_TIMER_STAGES stages — 0 query / filter / table
  *              preparation and windows, 1 the fast counting pass (MFMA tile,
  *              register tile or wave scan), 2 near-tie refinement and rank
  *              emission (pRotatE's three-call form: including the caller's
- *              host sin between the calls) — then the number of calls
- *              (n_out >= 4).
+ *              host sin between the calls) — then the number of DIRECTIONS
+ *              ranked (a kge_rank_filtered_both call counts 2) (n_out >= 4).
  * Not graph-capturable while enabled.
  */
 #define KGE_TIMER_STAGES 6

@@ -18,7 +18,7 @@ MODE_IDS = {"single": 0, "head-batch": 1, "tail-batch": 2}
 DEVERR_INDEX = 1
 DEVERR_SAMPLER = 2
 DEVERR_ARG = 4
-ABI_VERSION = "0.3"  # KGE_ABI_VERSION of the include/kge_hip.h this binding mirrors
+ABI_VERSION = "0.4"  # KGE_ABI_VERSION of the include/kge_hip.h this binding mirrors
 RANK_STAGE_LIST = 0x200  # KGE_RANK_STAGE_LIST
 RANK_FILTER_TABLE = 0x400  # KGE_RANK_FILTER_TABLE
 RANK_LIST_CAP = 1024  # KGE_RANK_LIST_CAP
@@ -142,6 +142,7 @@ SIGNATURES = {
     "kge_rank_workspace_bytes": (_SZ, [_DESC, _I64]),
     "kge_rank_filtered": (C.c_int, [_DESC, _I32, _P, _I64, _P, _P, _P, _P, _P, _SZ, _P, _P]),
     "kge_rank_filtered_ex": (C.c_int, [_DESC, _I32, _P, _I64, _P, _P, _P, _P, _P, _I32, _P, _SZ, _P, _P]),
+    "kge_rank_filtered_both": (C.c_int, [_DESC, _P, _I64, _P, _P, _P, _P, _P, _P, _P, _I32, _P, _SZ, _P, _P]),
     "kge_rank_sin_args": (C.c_int, [_DESC, _I32, _I64, _P, _P, _P, _SZ, _P, _P]),
     "kge_rank_finish_sin": (C.c_int, [_DESC, _I32, _I64, _P, _P, _P, _P, _P, _P, _SZ, _P, _P]),
     "kge_stage_timer": (C.c_int, [_I32, _P, _I32]),

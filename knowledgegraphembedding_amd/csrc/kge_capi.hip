@@ -178,9 +178,34 @@ struct StageTimer {
 };
 StageTimer g_timer;
 void timer_mark(hipStream_t s) { g_timer.mark(s); }
-// the ranking's stage timer (kge_stage_timer commands 4 / 5): KGE_RANK_TIMER_STAGES + 1
-// events per ranking call — start, fast pass begin, fast pass end, ranks written
-StageTimer g_rank_timer;
+// the ranking's stage timer (kge_stage_timer commands 4 / 5): marks tagged by
+// slot — 0 the call starts (with the call's number of directions), 1 fast pass
+// begins, 2 fast pass ends, 3 ranks written.  A call is the marks from one
+// slot-0 mark to the next; a stage is the time between the call's first mark of
+// its slot and its last mark of the next slot, so a call that writes ranks in
+// several pieces (pRotatE's per-chunk finish calls each mark slot 3) is timed to
+// its last piece, and the list stage's own calls need no padding.
+struct RankTimer {
+  bool on = false;
+  std::vector<hipEvent_t> ev;
+  std::vector<int> slot, ndir;
+  size_t used = 0;
+  void mark(hipStream_t s, int sl, int nd = 1) {
+    if (!on) return;
+    if (used == ev.size()) {
+      hipEvent_t e;
+      if (hipEventCreate(&e) != hipSuccess) return;
+      ev.push_back(e);
+      slot.push_back(0);
+      ndir.push_back(0);
+    }
+    if (hipEventRecord(ev[used], s) != hipSuccess) return;
+    slot[used] = sl;
+    ndir[used] = nd;
+    ++used;
+  }
+};
+RankTimer g_rank_timer;
 
 // ---- side stream: the index-only work (occurrence CSR) and the relation
 // pass run beside the gather kernels of the caller's stream.  Fork/join via
@@ -189,6 +214,7 @@ StageTimer g_rank_timer;
 struct Side {
   hipStream_t s = nullptr;
   hipEvent_t fork = nullptr, csr_done = nullptr, epi_done = nullptr, rel_done = nullptr;
+  hipEvent_t rk_fork = nullptr, rk_join = nullptr;  // ranking: the entity table's statistics / split beside the queries' stages
 };
 // Diagnostic switches, read per call so a test can flip them between calls;
 // none changes a result bit (each selects between paths that are tested
@@ -212,6 +238,8 @@ Side* side_for_device() {
     hipEventCreateWithFlags(&sd.csr_done, hipEventDisableTiming);
     hipEventCreateWithFlags(&sd.epi_done, hipEventDisableTiming);
     hipEventCreateWithFlags(&sd.rel_done, hipEventDisableTiming);
+    hipEventCreateWithFlags(&sd.rk_fork, hipEventDisableTiming);
+    hipEventCreateWithFlags(&sd.rk_join, hipEventDisableTiming);
   }
   return &sd;
 }
@@ -355,8 +383,16 @@ int run_grad(const kge_model_desc* m, const Geom& geo, int mode, const int64_t* 
   if (xstage == XS_CSR_ONLY) return launch_status(launch_csr(ca, s));  // kge_train_csr
   if (from_rows) ra.fuse_epi = 0;  // the epilogue reads the gathered dL/dq (k_row_epi)
 
-  const bool use_csr = !csr_ready;
+  // KGE_CSR_SERIAL=1 (diagnostic, same bits): the CSR on the caller's stream
+  // before the row pass instead of beside it — what k_row gains without the
+  // side stream's kernels competing for its CU slots
+  const bool csr_serial = !csr_ready && env_int("KGE_CSR_SERIAL", 0) != 0;
+  const bool use_csr = !csr_ready && !csr_serial;
   if (phases & KGE_PHASE_ROWS) {
+  if (csr_serial) {
+    st = launch_status(launch_csr(ca, s));
+    if (st) return st;
+  }
   // fork point: the occurrence CSR needs only the batch indices (recorded
   // before anything else is queued, so the side stream never waits for the
   // row pass)
@@ -1007,12 +1043,16 @@ enum { RS_ALL = 0, RS_LIST = 1, RS_ARGS = 2, RS_FINISH = 3 };
 int rank_impl(const kge_model_desc* m, int32_t mode, const int64_t* queries, int64_t nq, const int64_t* filt_off,
               const int64_t* filt_ids, int64_t* ranks_out, int32_t* ties_out, int32_t* listed_out, int32_t path,
               void* workspace, size_t workspace_bytes, int32_t* err_flag, void* stream, int stage,
-              const int64_t* item_off, const float* sins, float* args) {
+              const int64_t* item_off, const float* sins, float* args, const int64_t* filt_off2 = nullptr,
+              const int64_t* filt_ids2 = nullptr, int both = 0) {
   Geom geo;
   int st = check_model(m, &geo);
   if (st) return st;
-  if (mode != KGE_HEAD_BATCH && mode != KGE_TAIL_BATCH) return KGE_ERR_MODE;
+  // both: head-batch then tail-batch of the same queries in one pass (kge_rank_filtered_both);
+  // per-query arrays hold 2·nq entries, the head direction's first
+  if (!both && mode != KGE_HEAD_BATCH && mode != KGE_TAIL_BATCH) return KGE_ERR_MODE;
   if (!err_flag || nq < 0) return KGE_ERR_ARG;
+  if (both && (stage != RS_ALL || !filt_off2)) return KGE_ERR_ARG;
   if (stage == RS_ALL || stage == RS_LIST) {
     if (!queries || !filt_off) return KGE_ERR_ARG;
   }
@@ -1034,16 +1074,28 @@ int rank_impl(const kge_model_desc* m, int32_t mode, const int64_t* queries, int
   // RotatE's reference cos | sin table (read with the row's slot geometry)
   const float* trig = (m->model == KGE_ROTATE) ? m->relation_trig : nullptr;
   if (trig && geo.vec == 4 && !aligned16(trig)) return KGE_ERR_ARG;
+  const int ndir = both ? 2 : 1;
+  const int64_t nqt = ndir * nq;  // queries in the workspace
+  const int modes[2] = {both ? (int)KGE_HEAD_BATCH : (int)mode, (int)KGE_TAIL_BATCH};
+  const int64_t* const foff[2] = {filt_off, filt_off2};
+  const int64_t* const fids[2] = {filt_ids, filt_ids2};
   size_t need = 0;
-  RankWs w = carve_rank(workspace, m, nq, &need);
+  RankWs w = carve_rank(workspace, m, nqt, &need);
   if (!workspace || workspace_bytes < need) return KGE_ERR_WORKSPACE;
   hipStream_t s = as_stream(stream);
   // (gt, eq, gtx, eqx, ucnt are zeroed by k_rank_prep: RankArgs.zero_counts)
   const ModelOps& ops = ops_for(m->model);
   const bool cplx = (m->model == KGE_ROTATE || m->model == KGE_COMPLEX);
   const int K = cplx ? m->entity_dim / 2 : m->entity_dim;
+  const int64_t Le = m->entity_dim, W = (m->nentity + 31) / 32;
   RankWin win;
   win.delta = w.delta; win.ucnt = w.ucnt; win.ulist = w.ulist; win.cap = RANK_CAP;
+  // the per-query arrays of direction d start o = d·nq entries in
+  auto win_at = [&](int64_t o) {
+    RankWin x = win;
+    x.delta += o; x.ucnt += o; x.ulist += o * RANK_CAP;
+    return x;
+  };
 
   // 1. q, true ids (and, for the wave scan, s_true)
   RankArgs a;
@@ -1054,10 +1106,18 @@ int rank_impl(const kge_model_desc* m, int32_t mode, const int64_t* queries, int
   a.filt_off = filt_off; a.filt_ids = filt_ids;
   a.cpw = 64;
   a.q = w.q; a.s_true = w.s_true; a.true_id = w.true_id; a.gt = w.gt;
-  a.fbits = w.bits; a.W = (m->nentity + 31) / 32; a.win = win; a.err = err_flag;
+  a.fbits = w.bits; a.W = W; a.win = win; a.err = err_flag;
   a.prep_only = 1;
   a.zero_counts = 1;
+  a.cstride = nqt;
   a.trig = trig;
+  auto rank_at = [&](int d) {
+    RankArgs x = a;
+    const int64_t o = d * nq;
+    x.q += o * Le; x.s_true += o; x.true_id += o; x.gt += o; x.fbits += o * W; x.win = win_at(o);
+    x.filt_off = foff[d]; x.filt_ids = fids[d];
+    return x;
+  };
   // the refinement's arguments (stages 4 and 6)
   RefArgs ra;
   memset(&ra, 0, sizeof(ra));
@@ -1086,24 +1146,41 @@ int rank_impl(const kge_model_desc* m, int32_t mode, const int64_t* queries, int
   // slab's three chained MFMAs 97.6, the running sum 1.02·nslab
   const int64_t xns = xsplit_nslab(m->entity_dim);
   ra.fast_u = (rp != RP_MFMA) ? 0.f : (float)(513.2 + 258.1 + 97.6 + 1.02 * xns);
+  auto ref_at = [&](int d) {
+    RefArgs x = ra;
+    const int64_t o = d * nq;
+    x.q += o * Le; x.qref += o * Le; x.true_id += o; x.s_true += o; x.sref_true += o; x.s_true_w += o;
+    x.delta += o; x.ucnt += o; x.ulist += o * RANK_CAP; x.fbits += o * W;
+    x.gt += o; x.eq += o; x.gtx += o; x.eqx += o; x.sref_hi += o; x.done += o;
+    return x;
+  };
+  // one launch per direction of a mode-dependent stage (one direction unless both)
+  auto per_dir = [&](auto&& launch) -> int {
+    for (int d = 0; d < ndir; ++d) {
+      const int r = launch(d, modes[d]);
+      if (r) return r;
+    }
+    return KGE_OK;
+  };
   if (stage == RS_ARGS) return launch_status(ops.rank_ref(mode, 3, ra, s));
   EmitArgs ea;
   ea.gt = w.gt; ea.eq = w.eq; ea.gtx = w.gtx; ea.eqx = w.eqx; ea.ucnt = w.ucnt; ea.true_id = w.true_id;
-  ea.nq = nq; ea.cap = RANK_CAP; ea.ranks = ranks_out; ea.ties = ties_out; ea.listed = listed_out;
+  ea.nq = nqt; ea.cap = RANK_CAP; ea.ranks = ranks_out; ea.ties = ties_out; ea.listed = listed_out;
   ea.ltag = nullptr;
   for (int k = 0; k < 3; ++k) ea.ltag_v[k] = ltag_v[k];
 
   if (stage != RS_FINISH) {
-    g_rank_timer.mark(s);  // (rank timer) 0: the call starts
-    st = launch_status(ops.rank(mode, geo.vec, geo.ns, a, s));
-    if (st) return st;
-    // 2. excluded candidates (filtered ids + the true id) as a bitmap
-    if (ftab)
-      st = launch_status(launch_filter_bits_tab(queries, mode == KGE_HEAD_BATCH ? 1 : 0, filt_off, filt_ids, w.true_id,
-                                                nq, m->nentity, m->nrelation, w.bits, err_flag, s));
-    else
-      st = launch_status(launch_filter_bits(filt_off, filt_ids, w.true_id, nq, m->nentity, w.bits, err_flag, s));
-    if (st) return st;
+    g_rank_timer.mark(s, 0, ndir);  // (rank timer) 0: the call starts
+    // the entity table's work (tag, statistics, split or phase table) depends
+    // on the table alone.  KGE_RANK_SIDE=1 (diagnostic, same bits) runs it on
+    // the side stream beside the queries' q / bitmap / split (forked here,
+    // joined before the windows read the statistics): measured 1-2 % SLOWER
+    // than one stream (a ~130 µs dispatch gap before the counting tile after
+    // the cross-stream join; profiles/r06/rank), so the default is the
+    // caller's stream, the table's work queued first
+    Side* rsd = env_int("KGE_RANK_SIDE", 0) != 0 ? side_for_device() : nullptr;
+    hipStream_t ts = rsd ? rsd->s : s;
+    if (rsd) hipEventRecord(rsd->rk_fork, s);
     // the table's statistics and split operands: reused only where the tag
     // says this workspace already holds them for this table (k_rank_tag)
     const bool need_stats = (m->model == KGE_DISTMULT || m->model == KGE_COMPLEX || m->model == KGE_PROTATE);
@@ -1113,14 +1190,37 @@ int rank_impl(const kge_model_desc* m, int32_t mode, const int64_t* queries, int
     const float kappa = a.c.kappa_p;
     int64_t kbits = 0;
     memcpy(&kbits, &kappa, sizeof(kappa));
+    if (rsd) hipStreamWaitEvent(ts, rsd->rk_fork, 0);
     st = launch_status(launch_rank_tag(w.tag, m->entity_embedding, m->nentity, m->entity_dim, reuse ? 1 : 0,
                                        need_stats ? 1 : 0, rp == RP_MFMA ? 1 : (prot_tile ? 2 : 0),
-                                       prot_tile ? kbits : 0, s));
+                                       prot_tile ? kbits : 0, ts));
     if (st) return st;
     if (need_stats) {
-      st = launch_status(launch_table_stats(m->entity_embedding, m->nentity, m->entity_dim, w.stats, s, w.tag + 5));
+      st = launch_status(launch_table_stats(m->entity_embedding, m->nentity, m->entity_dim, w.stats, ts, w.tag + 5));
       if (st) return st;
     }
+    if (rp == RP_MFMA) {
+      st = launch_status(launch_split_bf16(m->entity_embedding, m->nentity, m->entity_dim, w.es, ts, w.tag + 6));
+      if (st) return st;
+    }
+    if (prot_tile) {
+      st = launch_status(launch_prot_phase(m->entity_embedding, m->nentity, K, kappa, 1, w.eph, ts, w.tag + 6));
+      if (st) return st;
+    }
+    if (rsd) hipEventRecord(rsd->rk_join, ts);
+    st = per_dir([&](int d, int md) { return launch_status(ops.rank(md, geo.vec, geo.ns, rank_at(d), s)); });
+    if (st) return st;
+    // 2. excluded candidates (filtered ids + the true id) as a bitmap
+    st = per_dir([&](int d, int md) {
+      const int64_t o = d * nq;
+      if (ftab)
+        return launch_status(launch_filter_bits_tab(queries, md == KGE_HEAD_BATCH ? 1 : 0, foff[d], fids[d],
+                                                    w.true_id + o, nq, m->nentity, m->nrelation, w.bits + o * W,
+                                                    err_flag, s));
+      return launch_status(launch_filter_bits(foff[d], fids[d], w.true_id + o, nq, m->nentity, w.bits + o * W,
+                                              err_flag, s));
+    });
+    if (st) return st;
     // 3. the fast pass's own s_true (same instruction sequence as its candidates)
     TileArgs ta;
     ta.q = w.q; ta.ent = m->entity_embedding; ta.modulus = m->modulus;
@@ -1128,9 +1228,15 @@ int rank_impl(const kge_model_desc* m, int32_t mode, const int64_t* queries, int
     ta.c = a.c; ta.true_id = w.true_id; ta.s_true = w.s_true;
     ta.fbits = w.bits; ta.W = a.W; ta.gt = w.gt; ta.win = win;
     ta.qph = w.qph; ta.eph = w.eph;
+    auto tile_at = [&](int d) {
+      TileArgs x = ta;
+      const int64_t o = d * nq;
+      x.q += o * Le; x.true_id += o; x.s_true += o; x.fbits += o * W; x.gt += o; x.win = win_at(o);
+      if (x.qph) x.qph += o * 2 * (int64_t)K;
+      return x;
+    };
     if (prot_tile) {
-      st = launch_status(launch_prot_phase(w.q, nq, K, 0.f, 0, w.qph, s));
-      if (!st) st = launch_status(launch_prot_phase(m->entity_embedding, m->nentity, K, kappa, 1, w.eph, s, w.tag + 6));
+      st = launch_status(launch_prot_phase(w.q, nqt, K, 0.f, 0, w.qph, s));
       if (st) return st;
     }
     // s_true in the reference's order after the window (k_rank_true_ref):
@@ -1141,43 +1247,50 @@ int rank_impl(const kge_model_desc* m, int32_t mode, const int64_t* queries, int
     // error only
     const bool true_ref = rp == RP_MFMA || (rp == RP_TILE && (m->model == KGE_ROTATE || prot_tile));
     if (rp == RP_MFMA) {
-      st = launch_status(launch_split_bf16(w.q, nq, m->entity_dim, w.qs, s));
-      if (!st)
-        st = launch_status(launch_split_bf16(m->entity_embedding, m->nentity, m->entity_dim, w.es, s, w.tag + 6));
+      // (q of both directions split in one launch: the tile is mode-independent)
+      st = launch_status(launch_split_bf16(w.q, nqt, m->entity_dim, w.qs, s));
+      if (rsd) hipStreamWaitEvent(s, rsd->rk_join, 0);  // join: everything below reads the table's work
       if (!st && !true_ref)
-        st = launch_status(launch_rank_mfma_x(1, w.qs, w.es, nq, m->nentity, m->entity_dim, w.true_id, w.s_true,
+        st = launch_status(launch_rank_mfma_x(1, w.qs, w.es, nqt, m->nentity, m->entity_dim, w.true_id, w.s_true,
                                               w.bits, w.gt, win, s));
-    } else if (rp == RP_MFMA32)
-      st = launch_status(launch_rank_mfma(1, w.q, m->entity_embedding, nq, m->nentity, m->entity_dim, w.true_id,
-                                          w.s_true, w.bits, w.gt, win, s));
-    else if (rp == RP_TILE)
-      st = launch_status(ops.rank_tile(mode, 1, ta, s));
+    } else {
+      if (rsd) hipStreamWaitEvent(s, rsd->rk_join, 0);  // join: everything below reads the table's work
+      if (rp == RP_MFMA32)
+        st = launch_status(launch_rank_mfma(1, w.q, m->entity_embedding, nqt, m->nentity, m->entity_dim, w.true_id,
+                                            w.s_true, w.bits, w.gt, win, s));
+      else if (rp == RP_TILE)
+        st = per_dir([&](int d, int md) { return launch_status(ops.rank_tile(md, 1, tile_at(d), s)); });
+    }
     if (st) return st;
     // 4. near-tie windows and the reference-order q
     ra.true_exact = true_ref ? 1 : 0;
-    st = launch_status(ops.rank_ref(mode, 0, ra, s));
+    st = per_dir([&](int d, int md) { return launch_status(ops.rank_ref(md, 0, ref_at(d), s)); });
     if (st) return st;
     if (true_ref) {
-      st = launch_status(ops.rank_ref(mode, 4, ra, s));
+      st = per_dir([&](int d, int md) { return launch_status(ops.rank_ref(md, 4, ref_at(d), s)); });
       if (st) return st;
     }
-    // 5. fast counting pass: clear cases counted, near-ties listed
-    g_rank_timer.mark(s);  // (rank timer) 1: fast pass begins
+    // 5. fast counting pass: clear cases counted, near-ties listed (the MFMA
+    // tiles take both directions' queries in one launch)
+    g_rank_timer.mark(s, 1);  // (rank timer) 1: fast pass begins
     if (rp == RP_MFMA) {
-      st = launch_status(launch_rank_mfma_x(0, w.qs, w.es, nq, m->nentity, m->entity_dim, w.true_id, w.s_true,
+      st = launch_status(launch_rank_mfma_x(0, w.qs, w.es, nqt, m->nentity, m->entity_dim, w.true_id, w.s_true,
                                             w.bits, w.gt, win, s));
     } else if (rp == RP_MFMA32) {
-      st = launch_status(launch_rank_mfma(0, w.q, m->entity_embedding, nq, m->nentity, m->entity_dim, w.true_id,
+      st = launch_status(launch_rank_mfma(0, w.q, m->entity_embedding, nqt, m->nentity, m->entity_dim, w.true_id,
                                           w.s_true, w.bits, w.gt, win, s));
     } else if (rp == RP_TILE) {
-      st = launch_status(ops.rank_tile(mode, 0, ta, s));
+      st = per_dir([&](int d, int md) { return launch_status(ops.rank_tile(md, 0, tile_at(d), s)); });
     } else {
-      a.prep_only = 0;
-      a.zero_counts = 0;
-      st = launch_status(ops.rank(mode, geo.vec, geo.ns, a, s));
+      st = per_dir([&](int d, int md) {
+        RankArgs x = rank_at(d);
+        x.prep_only = 0;
+        x.zero_counts = 0;
+        return launch_status(ops.rank(md, geo.vec, geo.ns, x, s));
+      });
     }
     if (st) return st;
-    g_rank_timer.mark(s);  // (rank timer) 2: fast pass ends
+    g_rank_timer.mark(s, 2);  // (rank timer) 2: fast pass ends
     if (stage == RS_LIST) {  // the lists stay in the workspace for RS_ARGS / RS_FINISH
       // pRotatE: every listed candidate's score as an interval under any
       // library sin within one ulp, in the reference's order; those whose
@@ -1201,14 +1314,14 @@ int rank_impl(const kge_model_desc* m, int32_t mode, const int64_t* queries, int
   }
   // 6. refinement in the reference's operation order; exact rescan on overflow
   // (RS_FINISH: overflowed pRotatE windows were ranked by the list stage)
-  st = launch_status(ops.rank_ref(mode, 1, ra, s));
+  st = per_dir([&](int d, int md) { return launch_status(ops.rank_ref(md, 1, ref_at(d), s)); });
   if (st) return st;
   if (stage != RS_FINISH) {
-    st = launch_status(ops.rank_ref(mode, 2, ra, s));
+    st = per_dir([&](int d, int md) { return launch_status(ops.rank_ref(md, 2, ref_at(d), s)); });
     if (st) return st;
   }
   st = launch_status(launch_rank_emit(ea, s));
-  if (!st) g_rank_timer.mark(s);  // (rank timer) 3: ranks written
+  if (!st) g_rank_timer.mark(s, 3);  // (rank timer) 3: ranks written (the last of a call's marks counts)
   return st;
 }
 }  // namespace
@@ -1223,6 +1336,16 @@ int kge_rank_filtered_ex(const kge_model_desc* m, int32_t mode, const int64_t* q
   const int stage = (path & KGE_RANK_STAGE_LIST) ? RS_LIST : RS_ALL;
   return rank_impl(m, mode, queries, nq, filt_off, filt_ids, ranks_out, ties_out, listed_out, path, workspace,
                    workspace_bytes, err_flag, stream, stage, nullptr, nullptr, nullptr);
+}
+
+int kge_rank_filtered_both(const kge_model_desc* m, const int64_t* queries, int64_t nq,
+                           const int64_t* filt_off_head, const int64_t* filt_ids_head, const int64_t* filt_off_tail,
+                           const int64_t* filt_ids_tail, int64_t* ranks_out, int32_t* ties_out, int32_t* listed_out,
+                           int32_t path, void* workspace, size_t workspace_bytes, int32_t* err_flag, void* stream) {
+  if (path & KGE_RANK_STAGE_LIST) return KGE_ERR_ARG;  // pRotatE's three-call form is per direction
+  return rank_impl(m, KGE_HEAD_BATCH, queries, nq, filt_off_head, filt_ids_head, ranks_out, ties_out, listed_out,
+                   path, workspace, workspace_bytes, err_flag, stream, RS_ALL, nullptr, nullptr, nullptr,
+                   filt_off_tail, filt_ids_tail, 1);
 }
 
 int kge_selftest_sin(float range, int32_t* max_dist_out, void* stream) {
@@ -1268,23 +1391,44 @@ int kge_stage_timer(int32_t command, float* stage_ms_out, int32_t n_out) {
     g_rank_timer.used = 0;
     return KGE_OK;
   }
-  if (command == 5) {  // ranking calls: summed stage times + the number of calls
+  if (command == 5) {  // ranking calls: summed stage times + the number of directions ranked
     constexpr int NR = KGE_RANK_TIMER_STAGES + 1;
     if (!stage_ms_out || n_out < NR) return KGE_ERR_ARG;
     for (int k = 0; k < NR; ++k) stage_ms_out[k] = 0.f;
-    const size_t calls = g_rank_timer.used / NR;
-    for (size_t c = 0; c < calls; ++c) {
-      hipEvent_t* e = &g_rank_timer.ev[c * NR];
-      hipError_t err = hipEventSynchronize(e[NR - 1]);
-      if (err != hipSuccess) return hip_status(err);
-      for (int k = 0; k < KGE_RANK_TIMER_STAGES; ++k) {
-        float ms = 0.f;
-        err = hipEventElapsedTime(&ms, e[k], e[k + 1]);
-        if (err != hipSuccess) return hip_status(err);
-        stage_ms_out[k] += ms;
+    const RankTimer& t = g_rank_timer;
+    size_t i = 0;
+    int dirs = 0;
+    while (i < t.used) {
+      if (t.slot[i] != 0) {  // (marks before the first call start: none are recorded so)
+        ++i;
+        continue;
       }
+      size_t j = i + 1;
+      while (j < t.used && t.slot[j] != 0) ++j;
+      // the call's marks [i, j): first and last event of each slot
+      long first[NR], last[NR];
+      for (int k = 0; k < NR; ++k) first[k] = last[k] = -1;
+      for (size_t x = i; x < j; ++x) {
+        const int sl = t.slot[x];
+        if (sl < 0 || sl >= NR) continue;
+        if (first[sl] < 0) first[sl] = (long)x;
+        last[sl] = (long)x;
+      }
+      if (last[NR - 1] >= 0) {  // the call wrote its ranks
+        hipError_t err = hipEventSynchronize(t.ev[last[NR - 1]]);
+        if (err != hipSuccess) return hip_status(err);
+        for (int k = 0; k < KGE_RANK_TIMER_STAGES; ++k) {
+          if (first[k] < 0 || last[k + 1] < 0) continue;
+          float ms = 0.f;
+          err = hipEventElapsedTime(&ms, t.ev[first[k]], t.ev[last[k + 1]]);
+          if (err != hipSuccess) return hip_status(err);
+          stage_ms_out[k] += ms;
+        }
+        dirs += t.ndir[i];
+      }
+      i = j;
     }
-    stage_ms_out[KGE_RANK_TIMER_STAGES] = (float)calls;
+    stage_ms_out[KGE_RANK_TIMER_STAGES] = (float)dirs;
     return KGE_OK;
   }
   const size_t calls = g_timer.used / NS_;

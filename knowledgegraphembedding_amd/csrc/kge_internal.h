@@ -1,5 +1,6 @@
 // kge_internal.h — argument blocks shared by the host dispatcher and the kernels.
 #pragma once
+#include <cstdlib>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -165,6 +166,12 @@ __host__ __device__ inline unsigned ent_lead_blocks(const EntArgs& a) {
 // Near-tie window of the fast ranking passes (all three): a candidate whose
 // fast fp32 score lies within delta[q] of the query's fast true score is not
 // counted but listed for the reference-order refinement (kge_rank_ref.h).
+// a diagnostic switch read per launch: true when the variable is set to "0"
+inline bool env_flag_off(const char* name) {
+  const char* e = getenv(name);
+  return e && e[0] == '0' && e[1] == 0;
+}
+
 struct RankWin {
   const float* delta;  // [nq]
   int32_t* ucnt;       // [nq]  listed candidates (may exceed cap: overflow)
@@ -204,7 +211,9 @@ struct RankArgs {
   RankWin win;
   int32_t* err;
   int prep_only;        // launch k_rank_prep only (the MFMA / tile paths count on their own)
-  int zero_counts;      // k_rank_prep zeroes gt and the five [nq] counters after it (eq, gtx, eqx, ucnt, done)
+  int zero_counts;      // k_rank_prep zeroes gt and the five counters after it (eq, gtx, eqx, ucnt, done)
+  int64_t cstride;      // distance between those counter arrays (the workspace's query count: nq, or 2·nq
+                        // when both directions share one workspace and gt points into it)
   const float* trig;    // RotatE: [R, 2, Lr] reference cos | sin of the phases, or null
 };
 

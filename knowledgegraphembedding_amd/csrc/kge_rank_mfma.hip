@@ -299,6 +299,54 @@ __global__ __launch_bounds__(256) void k_filter_bits_tab(const int64_t* __restri
   }
 }
 
+// Both bitmaps in one pass per query, built in LDS: one 256-thread block per
+// query zeroes its W-word row in LDS, sets the true id's and the filtered
+// ids' bits there (LDS atomics), and writes the whole row out with coalesced
+// stores — no separate memset of the [nq, W] bitmap and no global atomics.
+// `tab` non-null: the filter index's dense key → start table (k_filter_bits_tab's
+// lookup, `head` picks the key); else per-query lists off / ids.
+__global__ __launch_bounds__(256) void k_filter_bits_lds(const int64_t* __restrict__ queries, int head,
+                                                         const int64_t* __restrict__ tab,
+                                                         const int64_t* __restrict__ off,
+                                                         const int64_t* __restrict__ ids,
+                                                         const int64_t* __restrict__ true_id, int64_t nq, int64_t E,
+                                                         int64_t R, int W, uint32_t* __restrict__ bits,
+                                                         int32_t* err) {
+  extern __shared__ uint32_t fb_row[];
+  const int64_t q = blockIdx.x;
+  const int tid = threadIdx.x;
+  for (int k = tid; k < W; k += 256) fb_row[k] = 0u;
+  __syncthreads();
+  const int64_t t = true_id[q];
+  if (tid == 0 && t >= 0 && t < E) atomicOr(&fb_row[t >> 5], 1u << (t & 31));
+  int64_t b = 0, e_ = 0;
+  if (tab) {
+    const int64_t h = queries[q * 3], r = queries[q * 3 + 1], tl = queries[q * 3 + 2];
+    if (h >= 0 && h < E && tl >= 0 && tl < E && r >= 0 && r < R) {  // (k_rank_prep flags bad ids)
+      const int64_t key = head ? r * E + tl : h * R + r;
+      b = tab[key];
+      e_ = tab[key + 1];
+    }
+  } else {
+    b = off[q];
+    e_ = off[q + 1];
+  }
+  for (int64_t p = b + tid; p < e_; p += 256) {
+    const int64_t e = ids[p];
+    if (e < 0 || e >= E) {
+      atomicOr(err, KGE_DEVERR_INDEX);
+      continue;
+    }
+    atomicOr(&fb_row[e >> 5], 1u << (e & 31));
+  }
+  __syncthreads();
+  uint32_t* dst = bits + q * (int64_t)W;
+  for (int k = tid; k < W; k += 256) dst[k] = fb_row[k];
+}
+
+// rows up to this many words go through k_filter_bits_lds (E ≤ 393,216)
+constexpr int FB_LDS_WORDS = 12288;
+
 // rank = 1 + #{strictly greater} (counted beyond the window + refined inside
 // it), or the exact rescan's count for an overflowed window
 __global__ __launch_bounds__(256) void k_rank_emit(EmitArgs a) {
@@ -705,9 +753,14 @@ __global__ __launch_bounds__(256, 3) void k_rank_mfma_x(XArgs a) {
 int launch_filter_bits(const int64_t* filt_off, const int64_t* filt_ids, const int64_t* true_id, int64_t nq,
                        int64_t E, uint32_t* bits, int32_t* err, hipStream_t s) {
   const int64_t W = (E + 31) / 32;
+  if (nq > 65535) return -1;
+  if (W <= FB_LDS_WORDS) {
+    hipLaunchKernelGGL(k_filter_bits_lds, dim3((unsigned)nq), dim3(256), (size_t)W * 4, s, nullptr, 0, nullptr,
+                       filt_off, filt_ids, true_id, nq, E, (int64_t)0, (int)W, bits, err);
+    return (int)hipGetLastError();
+  }
   hipError_t he = hipMemsetAsync(bits, 0, (size_t)nq * W * 4, s);
   if (he != hipSuccess) return (int)he;
-  if (nq > 65535) return -1;
   hipLaunchKernelGGL(k_filter_bits, dim3(4, (unsigned)nq), dim3(256), 0, s, filt_off, filt_ids, true_id, nq, E, W,
                      bits, err);
   return (int)hipGetLastError();
@@ -717,6 +770,11 @@ int launch_filter_bits_tab(const int64_t* queries, int head, const int64_t* tab,
                            const int64_t* true_id, int64_t nq, int64_t E, int64_t R, uint32_t* bits, int32_t* err,
                            hipStream_t s) {
   const int64_t W = (E + 31) / 32;
+  if (W <= FB_LDS_WORDS && nq <= 0x7fffffff) {
+    hipLaunchKernelGGL(k_filter_bits_lds, dim3((unsigned)nq), dim3(256), (size_t)W * 4, s, queries, head, tab,
+                       nullptr, vals, true_id, nq, E, R, (int)W, bits, err);
+    return (int)hipGetLastError();
+  }
   hipError_t he = hipMemsetAsync(bits, 0, (size_t)nq * W * 4, s);
   if (he != hipSuccess) return (int)he;
   hipLaunchKernelGGL(k_filter_bits_tab, dim3((unsigned)((nq + 3) / 4)), dim3(256), 0, s, queries, head, tab, vals,

@@ -529,7 +529,34 @@ class KGEModel(nn.Module):
         with torch.no_grad():
             trig = model._rank_rotation(dev)
             lsin = model._rank_library_sin()
-            for mode in ('head-batch', 'tail-batch'):
+            both = not lsin and os.environ.get("KGE_RANK_BOTH", "1") != "0"
+            if both:
+                # both directions of a block in one pass (kge_rank_filtered_both;
+                # its workspace holds 2 × the block); the filter as the dense
+                # device table when the index has one, else per-query lists
+                tabs = None
+                if os.environ.get("KGE_RANK_FILTER_TABLE", "1") != "0":
+                    tabs = (index.device_table('head-batch', dev), index.device_table('tail-batch', dev))
+                    tabs = None if tabs[0] is None or tabs[1] is None else tabs
+                heads, tails = [], []
+                bb = max(1, block // 2)
+                for b0 in range(0, len(triples), bb):
+                    q = triples[b0:b0 + bb]
+                    if tabs is not None:
+                        fh, ft = tabs
+                    else:
+                        fh, ft = (tuple(torch.from_numpy(x) for x in index.filter_csr(q, m))
+                                  for m in ('head-batch', 'tail-batch'))
+                    ranks, _ = ops.rank_filtered_both(desc, torch.from_numpy(q), fh, ft, dev, relation_trig=trig,
+                                                      reuse_table=b0 > 0, filter_table=tabs is not None)
+                    heads.append(ranks[:len(q)])
+                    tails.append(ranks[len(q):])
+                per_mode = [heads, tails]
+                # progress messages on the reference's batch cadence (head-batch batches, then tail-batch)
+                for step in range(total_steps):
+                    if step % test_log_steps == 0:
+                        logging.info('Evaluating the model... (%d/%d)' % (step, total_steps))
+            for mode in (() if both else ('head-batch', 'tail-batch')):
                 ranks_all = []
                 per_mode.append(ranks_all)
                 for b0 in range(0, len(triples), block):
@@ -574,10 +601,44 @@ class KGEModel(nn.Module):
         with torch.no_grad():
             trig = self._rank_rotation(dev, relation_trig)
             qd = None
+            use_table = os.environ.get("KGE_RANK_FILTER_TABLE", "1") != "0"
+            if not self._rank_library_sin() and os.environ.get("KGE_RANK_BOTH", "1") != "0":
+                # both directions in one pass (kge_rank_filtered_both): one
+                # MFMA counting launch over 2·nq queries, the table's statistics
+                # and split operands once, half the small launches
+                fh = index.device_table('head-batch', dev) if use_table else None
+                ft = index.device_table('tail-batch', dev) if fh is not None else None
+                tab_mode = ft is not None  # else per-query lists (fh / ft rebound to them below)
+                if tab_mode:
+                    qd = torch.from_numpy(np.ascontiguousarray(q)).pin_memory()  # copied right before the launch
+                else:
+                    (oh, ih), (ot, it) = index.filter_csr(q, 'head-batch'), index.filter_csr(q, 'tail-batch')
+                    parts = [q.reshape(-1), oh, ih if len(ih) else np.zeros(1, np.int64), ot,
+                             it if len(it) else np.zeros(1, np.int64)]
+                    flat = torch.from_numpy(np.concatenate(parts).astype(np.int64, copy=False)).pin_memory()
+                    flat = flat.to(dev, non_blocking=True)
+                    o = [3 * nq, 3 * nq + nq + 1]
+                    o += [o[1] + max(1, len(ih)), o[1] + max(1, len(ih)) + nq + 1]
+                    qd = flat[:3 * nq].view(nq, 3)
+                    fh, ft = (flat[o[0]:o[1]], flat[o[1]:o[2]]), (flat[o[2]:o[3]], flat[o[3]:])
+                # ranks and ties straight into one buffer, read back with the
+                # error flag in two copies (no packing kernel)
+                buf = torch.empty(6 * nq, dtype=torch.int32, device=dev)
+                ops.rank_filtered_both(self.desc(), qd, fh, ft, dev, path=path, relation_trig=trig,
+                                       filter_table=tab_mode, out=buf)
+                host = torch.empty(6 * nq + 1, dtype=torch.int32, pin_memory=True)
+                host[:6 * nq].copy_(buf, non_blocking=True)
+                host[6 * nq:].copy_(ops.state(dev).err, non_blocking=True)
+                torch.cuda.current_stream(dev).synchronize()
+                h = host.numpy()
+                ops.raise_device_error_value(dev, int(h[-1]))
+                r = h[:4 * nq].view(np.int64)
+                t = h[4 * nq:6 * nq]
+                return (r[:nq].copy(), t[:nq].copy()), (r[nq:].copy(), t[nq:].copy())
             for mode in ('head-batch', 'tail-batch'):
                 # a dense filter index is looked up on the device
                 # (KGE_RANK_FILTER_TABLE, uploaded once per index)
-                table = index.device_table(mode, dev) if os.environ.get("KGE_RANK_FILTER_TABLE", "1") != "0" else None
+                table = index.device_table(mode, dev) if use_table else None
                 if table is not None:
                     if qd is None:
                         qd = torch.from_numpy(np.ascontiguousarray(q)).pin_memory().to(dev, non_blocking=True)

@@ -419,6 +419,16 @@ def reference_rotation(relation: torch.Tensor, embedding_range: float) -> torch.
 RANK_REUSE_TABLE = 0x100  # kge_hip.h KGE_RANK_REUSE_TABLE
 
 
+def _check_filter_shape(desc, nq: int, off: torch.Tensor, filter_table: bool) -> None:
+    """The device reads filt_off at every query's key (whole index, E·R + 1
+    starts) or at q, q + 1 (per-query lists, nq + 1): a wrong-sized array is
+    an out-of-bounds read on the device, refused here."""
+    want = desc.nentity * desc.nrelation + 1 if filter_table else nq + 1
+    if off.dim() != 1 or off.numel() != want:
+        raise ValueError(f"filter offsets: {tuple(off.shape)}, expected [{want}] "
+                         f"({'the whole index, E·R + 1' if filter_table else 'per-query lists, nq + 1'})")
+
+
 def rank_filtered(desc: _lib.ModelDesc, mode: str, queries: torch.Tensor, filt_off: torch.Tensor,
                   filt_ids: torch.Tensor, dev, path: str = "auto", listed: bool = False,
                   relation_trig: Optional[torch.Tensor] = None, reuse_table: bool = False,
@@ -452,6 +462,7 @@ def rank_filtered(desc: _lib.ModelDesc, mode: str, queries: torch.Tensor, filt_o
         desc = _lib.ModelDesc.from_buffer_copy(desc)
         desc.relation_trig = relation_trig.data_ptr()
     q = _idx(queries, dev)
+    _check_filter_shape(desc, q.shape[0], filt_off, filter_table)
     off = _idx(filt_off, dev)
     ids = _idx(filt_ids, dev) if filt_ids.numel() else torch.zeros(1, dtype=torch.int64, device=dev)
     nq = q.shape[0]
@@ -482,6 +493,60 @@ def rank_filtered(desc: _lib.ModelDesc, mode: str, queries: torch.Tensor, filt_o
     return (ranks, ties, lst) if listed else (ranks, ties)
 
 
+def rank_filtered_both(desc: _lib.ModelDesc, queries: torch.Tensor, filt_head, filt_tail, dev, path: str = "auto",
+                       listed: bool = False, relation_trig: Optional[torch.Tensor] = None, reuse_table: bool = False,
+                       filter_table: bool = False, out: Optional[torch.Tensor] = None):
+    """Both directions of one evaluation in one pass (kge_rank_filtered_both):
+    ranks [2·nq] int64 and ties [2·nq] int32 — head-batch then tail-batch, the
+    same values as rank_filtered(mode="head-batch") then
+    rank_filtered(mode="tail-batch").  filt_head / filt_tail: each direction's
+    (filt_off, filt_ids), per-query lists or (filter_table) the whole index.
+    `queries` may be a (pinned) host tensor: it is copied right before the
+    launch, after the host-side preparation, so the device does not wait for
+    Python between the copy and the first kernel.  `out` (int32 [6·nq] on the
+    device): ranks and ties written into it as [ranks as int32 pairs | ties],
+    one buffer for the caller's single read-back.  Not for pRotatE with the
+    reference's library sin (per direction: rank_filtered's three-call form)."""
+    if path not in RANK_PATHS:
+        raise ValueError("rank path %s not supported" % path)
+    if relation_trig is not None:
+        shape = (desc.nrelation, 2, desc.relation_dim)
+        if (tuple(relation_trig.shape) != shape or relation_trig.dtype != torch.float32
+                or not relation_trig.is_contiguous() or relation_trig.device != dev):
+            raise ValueError(f"relation_trig: expected a contiguous float32 {shape} tensor on {dev}")
+        desc = _lib.ModelDesc.from_buffer_copy(desc)
+        desc.relation_trig = relation_trig.data_ptr()
+    nq = queries.shape[0]
+    _check_filter_shape(desc, nq, filt_head[0], filter_table)
+    _check_filter_shape(desc, nq, filt_tail[0], filter_table)
+    fl = []
+    for off, ids in (filt_head, filt_tail):
+        fl.append((_idx(off, dev), _idx(ids, dev) if ids.numel() else torch.zeros(1, dtype=torch.int64, device=dev)))
+    if out is None:
+        ranks = torch.empty(2 * nq, dtype=torch.int64, device=dev)
+        ties = torch.empty(2 * nq, dtype=torch.int32, device=dev)
+    else:
+        if out.dtype != torch.int32 or out.device != dev or out.numel() < 6 * nq or not out.is_contiguous():
+            raise ValueError("out: a contiguous int32 device tensor of at least 6·nq elements")
+        ranks, ties = out[:4 * nq].view(torch.int64), out[4 * nq:6 * nq]
+    lst = torch.empty(2 * nq, dtype=torch.int32, device=dev) if listed else None
+    lib = _lib.load()
+    need = lib.kge_rank_workspace_bytes(desc, 2 * nq)
+    st = state(dev)
+    key = (desc.entity_embedding, desc.nentity, desc.entity_dim, desc.model)
+    prev = st.rank_ws_ptr
+    ws = st.workspace(need)
+    reuse_table = reuse_table and prev == (ws.data_ptr(),) + key
+    st.rank_ws_ptr = (ws.data_ptr(),) + key
+    flags = RANK_PATHS[path] | (RANK_REUSE_TABLE if reuse_table else 0) | (_lib.RANK_FILTER_TABLE if filter_table else 0)
+    q = _idx(queries, dev)  # (a pinned host tensor: its copy queues right before the launch)
+    _lib.check(lib.kge_rank_filtered_both(desc, q.data_ptr(), nq, fl[0][0].data_ptr(), fl[0][1].data_ptr(),
+                                          fl[1][0].data_ptr(), fl[1][1].data_ptr(), ranks.data_ptr(), ties.data_ptr(),
+                                          _ptr(lst), flags, ws.data_ptr(), ws.numel(), st.err.data_ptr(), _stream(dev)),
+               "kge_rank_filtered_both")
+    return (ranks, ties, lst) if listed else (ranks, ties)
+
+
 def reference_sin(args: torch.Tensor) -> torch.Tensor:
     """sin of pRotatE phase sums as the reference evaluates them: its own
     `torch.sin` on the CPU (model.py:245; ATen's vectorized CPU kernel — MKL
@@ -490,6 +555,18 @@ def reference_sin(args: torch.Tensor) -> torch.Tensor:
     arguments are batched (tests/test_rank_parity_gpu.py checks this host's
     bits against the reference's, tests/golden/protate_sin.npz)."""
     return torch.sin(args)
+
+
+def device_sin_queries(dev, reset: bool = True) -> int:
+    """pRotatE with the library sin: how many queries since the last reset the
+    list stage ranked with correctly rounded device sin instead (more
+    undecided candidates than RANK_LIST_CAP; each such call also logs a
+    warning).  0 means every pRotatE rank so far is the reference's bit for bit."""
+    st = state(dev)
+    n = st.__dict__.get("device_sin_queries", 0)
+    if reset:
+        st.__dict__["device_sin_queries"] = 0
+    return n
 
 
 SIN_CHUNK_BYTES = 256 << 20  # the host sin's argument buffer per round trip (pRotatE three-call form)
@@ -524,6 +601,17 @@ def _rank_protate_library_sin(lib, desc, mode_id, q, nq, off, ids, ranks, ties, 
     c_host.copy_(cnt, non_blocking=True)
     torch.cuda.current_stream(dev).synchronize()  # the counts size the argument buffers
     c = c_host.numpy().astype(np.int64)
+    # a query with more undecided candidates than a list (degenerate tables:
+    # > RANK_LIST_CAP near-identical rows) was ranked by the list stage on the
+    # device with correctly rounded sin, not the reference's library sin:
+    # counted, reported by the caller (KGEModel.rank_device_sin_queries) and logged
+    n_dev = int((c > _lib.RANK_LIST_CAP).sum())
+    st.__dict__["device_sin_queries"] = st.__dict__.get("device_sin_queries", 0) + n_dev
+    if n_dev:
+        import logging
+        logging.warning("pRotatE ranking: %d of %d queries had more than %d candidates within one ulp of the true "
+                        "score under any sin; they were ranked with correctly rounded sin on the device, not the "
+                        "reference's library sin", n_dev, nq, _lib.RANK_LIST_CAP)
     items = np.where((c >= 1) & (c <= _lib.RANK_LIST_CAP), 1 + c, 0)
     K = int(desc.entity_dim)
     per_q = items * K * 4

@@ -108,14 +108,18 @@ def test_rank_queries_both_directions_pipelined(name):
     assert np.array_equal(rt, rt1) and np.array_equal(tt, tt1)
 
 
+@pytest.mark.parametrize("ftab", ["1", "0"])
 @pytest.mark.parametrize("name", ["DistMult", "ComplEx", "pRotatE"])
-def test_test_step_query_blocks_reuse_the_table(name):
-    """test_step ranks in query blocks of at most 16384 and, from the second
+def test_test_step_query_blocks_reuse_the_table(name, ftab, monkeypatch):
+    """test_step ranks in query blocks (both directions of a block in one
+    pass, kge_rank_filtered_both, except pRotatE with the library sin; the
+    filter as the device table or, ftab = "0", per-query lists) and, from the second
     block (and direction) on, reuses the table statistics and split operands
     the first call left in the workspace (KGE_RANK_REUSE_TABLE); its ranks
     must equal one unblocked rank_queries call per direction without reuse.
     A training step between two evaluations must drop the reuse (the step
     writes the shared workspace and the table)."""
+    monkeypatch.setenv("KGE_RANK_FILTER_TABLE", ftab)
     E, R, d = 300, 7, 24
     m, *_ = build_model(name, E, R, d, 12.0, 9)
     g = np.random.default_rng(4)
@@ -173,10 +177,13 @@ def test_protate_degenerate_table_library_sin(kind, mode, monkeypatch):
 
     monkeypatch.setattr(torch, "sin", counting_sin)
     m.rank_trig = "reference"
+    ops.device_sin_queries(DEV)  # reset
     ranks, ties, listed = m.rank_queries(q, true, mode, listed=True)
     monkeypatch.setattr(torch, "sin", real_sin)
     assert sum(calls) == 0, calls  # nothing left for the host sin
     assert (listed > 1024).all()
+    # those queries are reported as ranked without the library sin
+    assert ops.device_sin_queries(DEV) == len(q)
     m.rank_trig = "device"
     r_dev, t_dev = m.rank_queries(q, true, mode, path="scan")
     assert np.array_equal(ranks, r_dev) and np.array_equal(ties, t_dev)

@@ -119,6 +119,7 @@ def check(tag, name, mode, ranks, ties, ref, bound, exact=True):
 def run_case(tag, name, E, R, d, gamma, seed, queries, filters, refs, report):
     m, ent, rel, mod, rng = build(name, E, R, d, gamma, seed)
     trig = reference_trig(tag, rel, rng)[0] if name == "RotatE" else None
+    bases = {}
     for mode in ("head-batch", "tail-batch"):
         ref = refs(mode)
         nq = len(ref["rank"])
@@ -140,6 +141,7 @@ def run_case(tag, name, E, R, d, gamma, seed, queries, filters, refs, report):
             dec, tied, amb, diff, udiff = check(tag, name, mode, ranks, ties, ref, bound)
             report.append((tag, name, mode, path, nq, dec, tied, amb, diff, udiff, round(float(listed.mean()), 1),
                            int(listed.max())))
+        bases[mode] = base
         if name == "pRotatE":  # correctly rounded device sin: within the last-bit bound
             m.rank_trig = "device"
             ranks, ties, listed = m.rank_queries(qs, filters, mode, listed=True)
@@ -148,6 +150,17 @@ def run_case(tag, name, E, R, d, gamma, seed, queries, filters, refs, report):
             dec, tied, amb, diff, udiff = check(tag, name, mode, ranks, ties, ref, bound, exact=False)
             report.append((tag, name, mode, "auto/device-sin", nq, dec, tied, amb, diff, udiff,
                            round(float(listed.mean()), 1), int(listed.max())))
+    # both directions in one pass (rank_queries_both → kge_rank_filtered_both;
+    # pRotatE with the library sin stays per direction): every path's ranks
+    # and ties equal the per-direction calls' above, i.e. the reference's
+    nq = len(bases["head-batch"][0])
+    if nq == len(bases["tail-batch"][0]):
+        for path in dict.fromkeys(p.split("/")[0] for p in PATHS[name]):
+            (rh, th), (rt, tt) = m.rank_queries_both(queries[:nq], filters, path=path, relation_trig=trig)
+            for mode, r, t in (("head-batch", rh, th), ("tail-batch", rt, tt)):
+                assert np.array_equal(r, bases[mode][0]) and np.array_equal(t, bases[mode][1]), \
+                    f"{tag} {name} {mode} {path}: both-directions pass"
+            report.append((tag, name, "both", path, 2 * nq, "ranks and ties = per-direction"))
     del m
     torch.cuda.empty_cache()
 
@@ -337,12 +350,14 @@ def test_split_bf16_tile_wide_dynamic_range(name, d):
         assert np.array_equal(r0, r1) and np.array_equal(t0, t1), (name, mode)
 
 
-@pytest.mark.parametrize("name", ["DistMult", "ComplEx", "RotatE", "TransE"])
+@pytest.mark.parametrize("name", ["DistMult", "ComplEx", "RotatE", "TransE", "pRotatE"])
 def test_filter_table_matches_query_lists(name, monkeypatch):
     """KGE_RANK_FILTER_TABLE (rank_queries_both's default for a dense filter
     index: the device looks each query's filtered ids up in the whole index)
     gives the ranks and ties of per-query filter lists built on the host
-    (rank_queries), on a wn18rr-shaped synthetic graph with repeated keys."""
+    (rank_queries), on a wn18rr-shaped synthetic graph with repeated keys —
+    through rank_queries_both's two-direction pass (kge_rank_filtered_both),
+    with the table and with per-query lists, against one call per direction."""
     from knowledgegraphembedding_amd import synth
     from knowledgegraphembedding_amd.filters import FilterIndex
     E, R, d = 3000, 11, 64
@@ -353,6 +368,8 @@ def test_filter_table_matches_query_lists(name, monkeypatch):
     cplx = name in ("ComplEx", "RotatE")
     torch.manual_seed(3)
     m = KGEModel(name, E, R, d, 12.0, cplx, name == "ComplEx").to(DEV)
+    if name == "pRotatE":  # the device sin: rank_queries_both takes the two-direction pass (its register tile)
+        m.rank_trig = "device"
     (rh, th), (rt, tt) = m.rank_queries_both(test, index)
     assert index.device_table("head-batch", DEV) is not None
     ref_h = m.rank_queries(test, index, "head-batch")
