@@ -865,15 +865,19 @@ int launch_prot_phase(const float* src, int64_t rows, int K, float kappa, int en
 }
 
 // kge_selftest_sin: the largest distance, in floats, between the device sinf
-// and the correctly rounded sin over every float x with |x| ≤ range
+// and the correctly rounded sin over every float x with |x| ≤ range — against
+// both of sin_rn2's candidates where it cannot tell which one that is
 __global__ __launch_bounds__(256) void k_selftest_sin(uint32_t lim, int32_t* maxd) {
   const uint64_t n = (uint64_t)lim * 2;
   int32_t m = 0;
   for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
     const uint32_t bits = (uint32_t)(i >> 1) | ((i & 1) ? 0x80000000u : 0u);
     const float x = __int_as_float((int32_t)bits);
-    const int32_t d = float_ord(sin_fast(x)) - float_ord(sin_rn(x));
-    m = max(m, d < 0 ? -d : d);
+    float alt;
+    const float r = sin_rn2(x, &alt);
+    const int32_t f = float_ord(sin_fast(x));
+    const int32_t d = f - float_ord(r), da = f - float_ord(alt);
+    m = max(m, max(d < 0 ? -d : d, da < 0 ? -da : da));
   }
   for (int o = 32; o > 0; o >>= 1) m = max(m, __shfl_xor(m, o));
   if ((threadIdx.x & 63) == 0 && m > 0) atomicMax(maxd, m);

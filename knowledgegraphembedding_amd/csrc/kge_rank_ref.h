@@ -33,8 +33,24 @@
 
 namespace kge {
 
-// correctly rounded fp32 transcendentals (a double result rounded once)
+// fp32 transcendentals from double: the double result (within an ulp of
+// double) rounded to float — the correctly rounded float except when the
+// exact value lies within that ulp of a float midpoint, so always within one
+// float of it (abs_sin_bounds allows for that)
 __device__ __forceinline__ float sin_rn(float x) { return (float)sin((double)x); }
+// sin_rn and its possible alternative: the double sin y (within a few double
+// ulps of sin x) rounds to r; when y lies within 2^-50·|y| of the midpoint
+// between r and its neighbour on y's side, the correctly rounded float may be
+// that neighbour — returned in *alt (else *alt = r).  The correctly rounded
+// sin(x) is always r or *alt (sin_rn alone rounds twice).
+__device__ __forceinline__ float sin_rn2(float x, float* alt) {
+  const double y = sin((double)x);
+  const float r = (float)y;
+  const float nb = (y > (double)r) ? nextafterf(r, INFINITY) : nextafterf(r, -INFINITY);
+  const double mid = 0.5 * ((double)r + (double)nb);
+  *alt = (fabs(y - mid) <= ldexp(fabs(y), -50)) ? nb : r;
+  return r;
+}
 __device__ __forceinline__ float cos_rn(float x) { return (float)cos((double)x); }
 // correctly rounded sqrt, as ATen's: __builtin_sqrtf lowers to v_sqrt_f32 plus
 // the fma residual correction (the build keeps HIP's default correctly rounded
@@ -193,11 +209,14 @@ __device__ float ref_score_half(const float* __restrict__ q, const float* __rest
 // The device's own fp32 sinf, against the correctly rounded value, checked on
 // every float of the range (kge_selftest_sin; tests/test_rank_parity_gpu.py
 // runs it on each GPU box): at most SIN_FAST_D1 floats apart for |x| ≤
-// SIN_FAST_R1 and SIN_FAST_D2 for |x| ≤ SIN_FAST_R2 (ROCm 7.2: 1 and 2).  So
-// the correctly rounded r lies within that many floats of sinf(x), the
-// library's value within one more, and the interval is taken around sinf(x)
-// — no double-precision sin (the interval screen's cost) — except beyond
-// SIN_FAST_R2, where r is computed as before.
+// SIN_FAST_R1 and SIN_FAST_D2 for |x| ≤ SIN_FAST_R2 (ROCm 7.2: 1 and 2) —
+// measured against BOTH floats sin_rn2 cannot tell apart where the double sin
+// lies next to a float midpoint, so against the correctly rounded r whichever
+// it is (the double result rounded once more is not always r).  So
+// r lies within that many floats of sinf(x), the library's value within one
+// more, and the interval is taken around sinf(x) — no double-precision sin
+// (the interval screen's cost) — except beyond SIN_FAST_R2, where it is taken
+// around sin_rn2's one or two candidates, ±1 float.
 constexpr float SIN_FAST_R1 = 16.f, SIN_FAST_R2 = 65536.f;
 constexpr int SIN_FAST_D1 = 1, SIN_FAST_D2 = 2;
 __device__ __forceinline__ int32_t float_ord(float f) {  // monotone in f (±0 → 0)
@@ -216,10 +235,12 @@ __device__ __forceinline__ tf2 abs_sin_bounds(float x) {
     p = ord_float(o - j);
     n = ord_float(o + j);
   } else {
-    const float r = sin_rn(x);
+    float alt;
+    const float r = sin_rn2(x, &alt);
     if (r != r) return tf2{r, r};
-    p = nextafterf(r, -INFINITY);
-    n = nextafterf(r, INFINITY);
+    const int32_t o = float_ord(r), oa = float_ord(alt);
+    p = ord_float((o < oa ? o : oa) - 1);
+    n = ord_float((o > oa ? o : oa) + 1);
   }
   if (x != x) return tf2{x, x};
   if (p <= 0.f && n >= 0.f) return tf2{0.f, fmaxf(-p, n)};

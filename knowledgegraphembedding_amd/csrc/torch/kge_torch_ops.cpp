@@ -17,6 +17,7 @@
 // dtypes and shapes.  CPU tensors are refused — there is no CPU path.  Every
 // launch goes on the current HIP stream of the tensors' device; scratch comes
 // from the caching allocator on that stream.
+#include <cstdlib>
 #include <ATen/ATen.h>
 #include <ATen/core/op_registration/op_registration.h>
 #include <c10/core/DeviceGuard.h>
@@ -337,7 +338,9 @@ std::tuple<Tensor, Tensor> rank_filtered_cuda(const Tensor& entity, const Tensor
                  "kge_rank_filtered_ex (list)");
     const Tensor c = cnt.to(at::kCPU);  // sync: the counts size the argument buffers
     const int32_t* cp = c.data_ptr<int32_t>();
-    const int64_t K = d.entity_dim, budget = (int64_t)256 << 20;
+    // KGE_SIN_CHUNK_BYTES: the chunk budget (tests force several chunks with a small one)
+    const char* be = getenv("KGE_SIN_CHUNK_BYTES");
+    const int64_t K = d.entity_dim, budget = (be && atoll(be) > 0) ? (int64_t)atoll(be) : ((int64_t)256 << 20);
     auto items_of = [&](int64_t i) -> int64_t {
       return (cp[i] >= 1 && cp[i] <= KGE_RANK_LIST_CAP) ? 1 + (int64_t)cp[i] : 0;
     };

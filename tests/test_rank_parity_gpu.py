@@ -394,3 +394,26 @@ def test_device_sinf_within_declared_floats():
         out = torch.zeros(1, dtype=torch.int32, device=DEV)
         _lib.check(lib.kge_selftest_sin(rng, out.data_ptr(), ops._stream(DEV)), "kge_selftest_sin")
         assert int(out.item()) <= bound, (rng, int(out.item()))
+
+
+@pytest.mark.parametrize("name", ["TransE", "pRotatE"])
+def test_tile_staging_switch_same_ranks(name, monkeypatch):
+    """The register tile's round-6 staging for TransE / pRotatE (queries
+    pre-splatted, padded k-rows, pipelined LDS reads) and round 5's
+    (KGE_TILE_SPL=0, diagnostic) give the same ranks, ties and listed counts —
+    the same arithmetic in the same order."""
+    from knowledgegraphembedding_amd import synth
+    E, R, d = 3000, 11, 64
+    h, r, t = synth.randint(921, (12000,), E), synth.randint(922, (12000,), R), synth.randint(923, (12000,), E)
+    true = np.unique(np.stack([h, r, t], 1), axis=0)
+    test = true[synth.randint(924, (500,), len(true))]
+    torch.manual_seed(4)
+    m = KGEModel(name, E, R, d, 12.0, False, False).to(DEV)
+    m.rank_trig = "device"
+    for mode in ("head-batch", "tail-batch"):
+        a = m.rank_queries(test, true, mode, listed=True)
+        monkeypatch.setenv("KGE_TILE_SPL", "0")
+        b = m.rank_queries(test, true, mode, listed=True)
+        monkeypatch.delenv("KGE_TILE_SPL")
+        for x, y in zip(a, b):
+            assert np.array_equal(x, y), (name, mode)
