@@ -101,8 +101,7 @@ typedef struct kge_model_desc {
 /* Library identity: "knowledgegraphembedding_amd <KGE_ABI_VERSION> gfx950".  The
  * version changes with every change of a struct, a signature or a call
  * protocol in this header (0.3: pRotatE's three-call item counts; 0.4:
- * kge_rank_filtered_both, kge_train_step_ahead, the ranking timer counting
- * directions);
+ * kge_rank_filtered_both, the ranking timer counting directions);
  * loaders refuse a library whose version differs from the header they bind. */
 #define KGE_ABI_VERSION "0.4"
 const char *kge_version(void);
@@ -214,30 +213,6 @@ int kge_train_step(const kge_model_desc *m, int32_t mode, const int64_t *pos, co
                    float regularization, const kge_adam_desc *adam, float *grad_entity, float *grad_relation,
                    float *grad_modulus, float *losses_out, void *workspace, size_t workspace_bytes,
                    int32_t *err_flag, void *stream);
-/*
- * kge_train_step (adam non-null) or kge_train_step_grads (adam null) with the
- * NEXT batch's occurrence CSR built one step ahead (no reference counterpart:
- * the reference's train_step is model.py:252-312, one batch per call).  The
- * CSR needs only the batch's ids; building it beside the row pass (what the
- * one-call step does) puts its kernels next to the HBM-bound k_row, which runs
- * ~4 % slower for it.  Here:
- *   next_pos / next_neg [batch, nneg] / next_workspace (all non-null, or all
- *     null): after this step's row pass, the next batch's CSR is built into
- *     next_workspace (≠ workspace, sized like it) on the library's side stream,
- *     beside this step's entity pass; the batch must keep these shapes;
- *   csr_ready = 1: this call's batch and workspace are the previous call's
- *     next_* (KGE_ERR_ARG otherwise); its CSR is not rebuilt — the step waits
- *     for the look-ahead's and reads it.
- * Any other call on next_workspace in between voids the look-ahead (a later
- * csr_ready call returns KGE_ERR_ARG).  Bit-identical to kge_train_step.
- */
-int kge_train_step_ahead(const kge_model_desc *m, int32_t mode, const int64_t *pos, const int64_t *neg,
-                         int64_t batch, int64_t nneg, const float *subsampling_weight, const float *weight_sum,
-                         int32_t uni_weight, int64_t uni_batch, int32_t adversarial, float adversarial_temperature,
-                         float regularization, const kge_adam_desc *adam, float *grad_entity, float *grad_relation,
-                         float *grad_modulus, float *losses_out, void *workspace, size_t workspace_bytes,
-                         int32_t *err_flag, void *stream, int32_t csr_ready, const int64_t *next_pos,
-                         const int64_t *next_neg, void *next_workspace, size_t next_workspace_bytes);
 
 /*
  * Data-parallel FACTOR EXCHANGE (distributed.py, exchange "factors"): instead

@@ -109,11 +109,6 @@ SIGNATURES = {
         [_DESC, _I32, _P, _P, _I64, _I64, _P, _P, _I32, _I64, _I32, _F, _F, C.POINTER(AdamDesc), _P, _P, _P, _P, _P,
          _SZ, _P, _P],
     ),
-    "kge_train_step_ahead": (
-        C.c_int,
-        [_DESC, _I32, _P, _P, _I64, _I64, _P, _P, _I32, _I64, _I32, _F, _F, C.POINTER(AdamDesc), _P, _P, _P, _P, _P,
-         _SZ, _P, _P, _I32, _P, _P, _P, _SZ],
-    ),
     "kge_train_rows_slice": (
         C.c_int,
         [_DESC, _I32, _P, _P, _I64, _I64, _P, _P, _I32, _I64, _I32, _F, _P, _P, _P, _P, _SZ, _P, _P],

@@ -215,12 +215,6 @@ struct Side {
   hipStream_t s = nullptr;
   hipEvent_t fork = nullptr, csr_done = nullptr, epi_done = nullptr, rel_done = nullptr;
   hipEvent_t rk_fork = nullptr, rk_join = nullptr;  // ranking: the entity table's statistics / split beside the queries' stages
-  // training look-ahead (kge_train_step_ahead): the next batch's CSR, forked
-  // after this step's row pass, and the batch / workspace it was built for
-  hipEvent_t ahead_fork = nullptr, ahead_done = nullptr;
-  const int64_t *ahead_pos = nullptr, *ahead_neg = nullptr;
-  const void* ahead_ws = nullptr;
-  int64_t ahead_B = 0, ahead_n = 0;
 };
 // Diagnostic switches, read per call so a test can flip them between calls;
 // none changes a result bit (each selects between paths that are tested
@@ -246,8 +240,6 @@ Side* side_for_device() {
     hipEventCreateWithFlags(&sd.rel_done, hipEventDisableTiming);
     hipEventCreateWithFlags(&sd.rk_fork, hipEventDisableTiming);
     hipEventCreateWithFlags(&sd.rk_join, hipEventDisableTiming);
-    hipEventCreateWithFlags(&sd.ahead_fork, hipEventDisableTiming);
-    hipEventCreateWithFlags(&sd.ahead_done, hipEventDisableTiming);
   }
   return &sd;
 }
@@ -306,8 +298,7 @@ int run_grad(const kge_model_desc* m, const Geom& geo, int mode, const int64_t* 
              int64_t neg_stride, int64_t B, int64_t n, RowArgs ra, GradWs w, float* grad_entity,
              float* grad_relation, float* grad_modulus, float reg, FinArgs fa, const kge_adam_desc* adam,
              int32_t* err, hipStream_t s, int phases = KGE_PHASE_ALL, int64_t e_begin = 0, int64_t e_end = -1,
-             int xstage = XS_NONE, int reg_relations = 1, int64_t csr_lo = 0, int64_t csr_hi = -1,
-             const CsrArgs* next_csr = nullptr, int ahead_ready = 0) {
+             int xstage = XS_NONE, int reg_relations = 1, int64_t csr_lo = 0, int64_t csr_hi = -1) {
   const ModelOps& op = ops_for(m->model);
   AdamK ak;
   ak.b1 = adam ? adam->beta1 : 0.f;
@@ -395,18 +386,9 @@ int run_grad(const kge_model_desc* m, const Geom& geo, int mode, const int64_t* 
   // KGE_CSR_SERIAL=1 (diagnostic, same bits): the CSR on the caller's stream
   // before the row pass instead of beside it — what k_row gains without the
   // side stream's kernels competing for its CU slots
-  // ahead_ready: this batch's CSR was built by the previous call's look-ahead
-  // (kge_train_step_ahead) on the side stream; joined at the step's start
-  const bool csr_serial = !csr_ready && !ahead_ready && env_int("KGE_CSR_SERIAL", 0) != 0;
-  const bool use_csr = !csr_ready && !csr_serial && !ahead_ready;
+  const bool csr_serial = !csr_ready && env_int("KGE_CSR_SERIAL", 0) != 0;
+  const bool use_csr = !csr_ready && !csr_serial;
   if (phases & KGE_PHASE_ROWS) {
-  if (ahead_ready) {
-    // this batch's CSR, built during the previous step's entity pass: waited
-    // for here, before this call records the event again for the next batch
-    // (a wait takes the event's state when it is enqueued); normally long done
-    if (!sd) return KGE_ERR_ARG;
-    hipStreamWaitEvent(s, sd->ahead_done, 0);
-  }
   if (csr_serial) {
     st = launch_status(launch_csr(ca, s));
     if (st) return st;
@@ -449,18 +431,6 @@ int run_grad(const kge_model_desc* m, const Geom& geo, int mode, const int64_t* 
   }
   if (timed && !all)
     for (int k = 0; k < 3; ++k) g_timer.mark(s);  // stages 3-5 not in this call
-  // the next batch's CSR (kge_train_step_ahead) beside this step's entity
-  // pass — after the row pass, so k_row runs with no CSR kernels competing for
-  // its CU slots.  The side stream is in order: behind this step's own CSR
-  // and relation pass if it has them.
-  if (next_csr) {
-    if (!sd) return KGE_ERR_ARG;
-    hipEventRecord(sd->ahead_fork, s);
-    hipStreamWaitEvent(ss, sd->ahead_fork, 0);
-    st = launch_status(launch_csr(*next_csr, ss));
-    if (st) return st;
-    hipEventRecord(sd->ahead_done, ss);
-  }
   }  // KGE_PHASE_ROWS
 
   fa.row_stats = w.row_stats;
@@ -662,8 +632,7 @@ static int train_impl(const kge_model_desc* m, int32_t mode, const int64_t* pos,
                       float* losses_out, void* workspace, size_t workspace_bytes, int32_t* err_flag, void* stream,
                       int32_t phases = KGE_PHASE_ALL, int64_t e_begin = 0, int64_t e_end = -1, int xstage = XS_NONE,
                       float* rows_g = nullptr, float* rows_dq = nullptr, float* rows_stats = nullptr,
-                      int reg_relations = 1, int64_t csr_lo = 0, int64_t csr_hi = -1,
-                      const CsrArgs* next_csr = nullptr, int ahead_ready = 0) {
+                      int reg_relations = 1, int64_t csr_lo = 0, int64_t csr_hi = -1) {
   Geom geo;
   int st = check_model(m, &geo);
   if (st) return st;
@@ -724,13 +693,9 @@ static int train_impl(const kge_model_desc* m, int32_t mode, const int64_t* pos,
   if (phases < 1 || phases > KGE_PHASE_ALL) return KGE_ERR_ARG;
   if (e_end < 0) e_end = m->nentity;
   if (e_begin < 0 || e_begin > e_end || e_end > m->nentity) return KGE_ERR_ARG;
-  if (!ahead_ready) {  // this call overwrites its workspace: a look-ahead CSR left there is gone
-    Side* sd = side_for_device();
-    if (sd && sd->ahead_ws == workspace) sd->ahead_ws = nullptr;
-  }
   return run_grad(m, geo, mode, pos, neg, nneg, batch, nneg, ra, w, grad_entity, grad_relation,
                   m->model == KGE_PROTATE ? grad_modulus : nullptr, regularization, fa, adam, err_flag, s, phases,
-                  e_begin, e_end, xstage, reg_relations, csr_lo, csr_hi, next_csr, ahead_ready);
+                  e_begin, e_end, xstage, reg_relations, csr_lo, csr_hi);
 }
 
 int kge_train_rows_slice(const kge_model_desc* m, int32_t mode, const int64_t* pos, const int64_t* neg,
@@ -991,49 +956,6 @@ int kge_train_step(const kge_model_desc* m, int32_t mode, const int64_t* pos, co
   return train_impl(m, mode, pos, neg, batch, nneg, subsampling_weight, weight_sum, uni_weight, uni_batch, adversarial,
                     adversarial_temperature, regularization, adam, grad_entity, grad_relation, grad_modulus,
                     losses_out, workspace, workspace_bytes, err_flag, stream);
-}
-
-int kge_train_step_ahead(const kge_model_desc* m, int32_t mode, const int64_t* pos, const int64_t* neg,
-                         int64_t batch, int64_t nneg, const float* subsampling_weight, const float* weight_sum,
-                         int32_t uni_weight, int64_t uni_batch, int32_t adversarial, float adversarial_temperature,
-                         float regularization, const kge_adam_desc* adam, float* grad_entity, float* grad_relation,
-                         float* grad_modulus, float* losses_out, void* workspace, size_t workspace_bytes,
-                         int32_t* err_flag, void* stream, int32_t csr_ready, const int64_t* next_pos,
-                         const int64_t* next_neg, void* next_workspace, size_t next_workspace_bytes) {
-  Side* sd = side_for_device();
-  if (!sd || !m) return KGE_ERR_ARG;
-  // csr_ready: the previous call built exactly this batch's CSR into this workspace
-  if (csr_ready && (sd->ahead_ws != workspace || sd->ahead_pos != pos || sd->ahead_neg != neg ||
-                    sd->ahead_B != batch || sd->ahead_n != nneg))
-    return KGE_ERR_ARG;
-  const bool next = next_pos && next_neg && next_workspace;
-  if ((next_pos || next_neg || next_workspace) && !next) return KGE_ERR_ARG;
-  CsrArgs nc;
-  memset(&nc, 0, sizeof(nc));
-  if (next) {
-    if (next_workspace == workspace) return KGE_ERR_ARG;  // in use by this step
-    size_t need = 0;
-    GradWs nw = carve_grad(next_workspace, m, batch, nneg, &need);
-    if (next_workspace_bytes < need) return KGE_ERR_WORKSPACE;
-    nc.pos = next_pos; nc.neg = next_neg; nc.neg_stride = nneg;
-    nc.B = batch; nc.n = nneg; nc.Bn = batch * nneg; nc.E = m->nentity; nc.R = m->nrelation;
-    nc.keys = nw.keys; nc.cnt = nw.cnt; nc.off = nw.off; nc.tmp = nw.tmp; nc.occ = nw.occ; nc.err = err_flag;
-    nc.e_lo = 0; nc.e_hi = m->nentity;
-    nc.scan_tmp = nw.scan_tmp; nc.scan_tmp_bytes = nw.scan_tmp_bytes;
-  }
-  sd->ahead_ws = nullptr;  // until this call has queued the next CSR
-  const int r = train_impl(m, mode, pos, neg, batch, nneg, subsampling_weight, weight_sum, uni_weight, uni_batch,
-                           adversarial, adversarial_temperature, regularization, adam, grad_entity, grad_relation,
-                           grad_modulus, losses_out, workspace, workspace_bytes, err_flag, stream, KGE_PHASE_ALL, 0,
-                           -1, XS_NONE, nullptr, nullptr, nullptr, 1, 0, -1, next ? &nc : nullptr, csr_ready ? 1 : 0);
-  if (r == KGE_OK && next) {
-    sd->ahead_ws = next_workspace;
-    sd->ahead_pos = next_pos;
-    sd->ahead_neg = next_neg;
-    sd->ahead_B = batch;
-    sd->ahead_n = nneg;
-  }
-  return r;
 }
 
 int kge_weight_sum(const float* w, int64_t n, float* out, void* stream) {

@@ -231,13 +231,6 @@ class KGEModel(nn.Module):
         self.keep_grads = True
         # apply a KGEAdam update inside the gradient passes (kge_train_step)
         self.fuse_optimizer = True
-        # single-device train_step draws the next batch one step early and
-        # builds its occurrence CSR beside this step's entity pass
-        # (kge_train_step_ahead); False: each step builds its own beside its
-        # row pass.  Same batches in the same order, same bits.
-        self.csr_ahead = os.environ.get("KGE_CSR_AHEAD", "1") != "0"
-        self._pending = {}  # id(iterator) -> (iterator, the batch the look-ahead drew from it)
-        self._ahead_ws = None  # this model's two look-ahead workspaces (ops.ahead_workspaces)
         # RotatE / pRotatE ranking: the reference's own CPU trig ("reference":
         # RotatE's queries rotated by its cos / sin of the relation phases,
         # ops.reference_rotation; pRotatE's near-ties re-scored from its sin
@@ -393,7 +386,7 @@ class KGEModel(nn.Module):
 
     def compute_train_grads(self, positive_sample, negative_sample, subsampling_weight, mode, args,
                             weight_sum=None, uni_batch=0, optimizer=None, entity_chunks=None, on_entity_chunk=None,
-                            losses_out=None, ahead=None):
+                            losses_out=None):
         """Fused forward + self-adversarial loss + backward (model.py:268-301).
         Writes dense .grad tensors; returns the device [5] vector
         (positive_sample_loss, negative_sample_loss, loss, regularization, error flag).
@@ -402,10 +395,7 @@ class KGEModel(nn.Module):
         With `entity_chunks` [(e0, e1), ...] the entity-gradient pass runs one
         row range at a time and `on_entity_chunk(e0, e1, grad_entity)` is called
         as soon as each range is queued (the data-parallel path starts that
-        range's all-reduce there, overlapping the next range's computation).
-        With `ahead` (workspace, csr_ready, next (pos, neg) or None, next
-        workspace) the step runs as kge_train_step_ahead (train_step's CSR
-        look-ahead)."""
+        range's all-reduce there, overlapping the next range's computation)."""
         dev = ops._require_device(self.entity_embedding)
         g, rng = self._host_scalars()
         ge, gr, gm, losses = self._grad_buffers()
@@ -421,11 +411,7 @@ class KGEModel(nn.Module):
                   grad_entity=ge, grad_relation=gr, grad_modulus=gm, losses=losses,
                   weight_sum_dev=weight_sum, uni_batch=uni_batch)
         desc = self.desc()
-        if ahead is not None:
-            ws, ready, nxt, nws = ahead
-            ops.train_step_ahead(desc, mode, positive_sample, negative_sample, subsampling_weight, dev, adam=adam,
-                                 workspace=ws, csr_ready=ready, next_batch=nxt, next_workspace=nws, **kw)
-        elif entity_chunks is None:
+        if entity_chunks is None:
             ops.train_step_grads(desc, mode, positive_sample, negative_sample, subsampling_weight, dev, adam=adam,
                                  **kw)
         else:
@@ -445,29 +431,6 @@ class KGEModel(nn.Module):
             self.modulus.grad = gm
         return losses
 
-    # ------------------------------------------------- batch look-ahead
-    @staticmethod
-    def _draw(it, dev):
-        """The iterator's next batch on `dev` (None when it is exhausted)."""
-        try:
-            p, n, w, mode = next(it)
-        except StopIteration:
-            return None
-        return (p.to(dev, non_blocking=True).long().contiguous(), n.to(dev, non_blocking=True).long().contiguous(),
-                w.to(dev, non_blocking=True), mode)
-
-    def _take(self, it, dev):
-        """This step's batch: the one the look-ahead already drew from this
-        iterator, if any (kept per iterator, so switching iterators loses no
-        batch), else the iterator's next."""
-        a = self._pending.pop(id(it), None)
-        if a is not None and a[0] is it:
-            return a[1]
-        b = self._draw(it, dev)
-        if b is None:
-            raise StopIteration
-        return b
-
     @staticmethod
     def train_step(model, optimizer, train_iterator, args):
         '''
@@ -481,38 +444,14 @@ class KGEModel(nn.Module):
         '''
         model.train()
         optimizer.zero_grad()
+        positive_sample, negative_sample, subsampling_weight, mode = next(train_iterator)
         dev = model.entity_embedding.device
+        positive_sample = positive_sample.to(dev, non_blocking=True)
+        negative_sample = negative_sample.to(dev, non_blocking=True)
+        subsampling_weight = subsampling_weight.to(dev, non_blocking=True)
+
         part = getattr(model, 'row_partition', None)
         dp = getattr(args, 'dp_group', None)
-        ahead = None
-        if part is None and dp is None and model.csr_ahead and dev.type == 'cuda':
-            # the next batch is drawn one step early, so its occurrence CSR is
-            # built beside this step's entity pass (kge_train_step_ahead) and
-            # not beside the next step's HBM-bound row pass; batches are used
-            # in the iterator's order, one per call, as before
-            cur = model._take(train_iterator, dev)
-            positive_sample, negative_sample, subsampling_weight, mode = cur
-            nxt = model._draw(train_iterator, dev)
-            if nxt is not None:
-                model._pending[id(train_iterator)] = (train_iterator, nxt)
-            same = nxt is not None and nxt[0].shape == positive_sample.shape and \
-                nxt[1].shape == negative_sample.shape
-            model._ahead_ws = ops.ahead_workspaces(model.desc(), negative_sample.shape[0],
-                                                   negative_sample.shape[1], dev, model._ahead_ws)
-            # the library keeps one look-ahead CSR per device: ready only if it
-            # is still the one built for exactly this batch (ops.ahead_owner)
-            token = id(model._ahead_ws[0])
-            owner = ops.ahead_owner(dev)
-            ready = owner is not None and owner[:3] == (token, positive_sample.data_ptr(), negative_sample.data_ptr())
-            ws = owner[3] if ready else 0
-            ws_t, ws_n = model._ahead_ws[ws], model._ahead_ws[1 - ws]
-            ahead = (ws_t, ready, (nxt[0], nxt[1]) if same else None, ws_n if same else None)
-            ops.ahead_owner(dev, (token, nxt[0].data_ptr(), nxt[1].data_ptr(), 1 - ws) if same else ())
-        else:
-            positive_sample, negative_sample, subsampling_weight, mode = model._take(train_iterator, dev)
-            if dev.type == 'cuda':
-                ops.ahead_owner(dev, ())  # a look-ahead CSR is claimed by no batch any more
-
         if part is not None:
             # row-partitioned entity table (partition.py): reduce-scatter to the owners
             losses = part.train_grads(model, positive_sample, negative_sample, subsampling_weight, mode, args,
@@ -534,7 +473,7 @@ class KGEModel(nn.Module):
             # other optimizer sees ordinary dense .grad tensors.  The loss
             # vector goes straight into the next pinned log slot (no D2H copy)
             losses = model.compute_train_grads(positive_sample, negative_sample, subsampling_weight, mode, args,
-                                               optimizer=optimizer, losses_out=model._log_slot(dev), ahead=ahead)
+                                               optimizer=optimizer, losses_out=model._log_slot(dev))
 
         optimizer.step()
         if part is not None:

@@ -234,69 +234,6 @@ def train_step_grads(desc: _lib.ModelDesc, mode: str, pos: torch.Tensor, neg: to
         _lib.check(lib.kge_train_step(*common, adam, *tail), "kge_train_step")
 
 
-def ahead_workspaces(desc: _lib.ModelDesc, B: int, n: int, dev, pair=None):
-    """Two training workspaces of the caller's own for the look-ahead step
-    (kge_train_step_ahead alternates them: step t runs in one while the next
-    batch's CSR is built into the other); `pair` is the caller's current
-    pair, returned as is while it is large enough."""
-    lib = _lib.load()
-    key = (desc.entity_dim, desc.relation_dim, desc.nentity, desc.nrelation, B, n)
-    need = _WS_BYTES.get(key)
-    if need is None:
-        need = _WS_BYTES[key] = lib.kge_train_workspace_bytes(desc, B, n)
-    if pair is None or pair[0].numel() < need or pair[0].device != dev:
-        if pair is not None:
-            torch.cuda.synchronize(pair[0].device)  # the old pair may still be read on either stream
-        pair = tuple(torch.empty(need + 4096, dtype=torch.uint8, device=dev) for _ in range(2))
-    return pair
-
-
-def ahead_owner(dev, owner=None):
-    """The library keeps ONE look-ahead CSR per device (the last
-    kge_train_step_ahead's next batch): (caller token, pos and neg data
-    pointers, workspace index) of the batch it was built for, () for none.
-    With `owner`: record it.  A batch that does not match builds its CSR
-    again (csr_ready = 0)."""
-    st = state(dev)
-    if owner is not None:
-        st.__dict__["ahead_owner"] = owner
-    return st.__dict__.get("ahead_owner")
-
-
-def train_step_ahead(desc: _lib.ModelDesc, mode: str, pos: torch.Tensor, neg: torch.Tensor, sub_w: torch.Tensor,
-                     dev, *, adversarial: bool, temperature: float, uni_weight: bool, regularization: float,
-                     grad_entity: torch.Tensor, grad_relation: torch.Tensor, grad_modulus: Optional[torch.Tensor],
-                     losses: torch.Tensor, workspace: torch.Tensor, csr_ready: bool,
-                     next_batch: Optional[tuple] = None, next_workspace: Optional[torch.Tensor] = None,
-                     weight_sum_dev: Optional[torch.Tensor] = None, uni_batch: int = 0,
-                     adam: Optional[_lib.AdamDesc] = None) -> None:
-    """train_step_grads (adam: the fused step) with the next batch's CSR built
-    one step ahead (kge_train_step_ahead): `next_batch` (pos, neg) device
-    tensors of the same shapes, built into `next_workspace` beside this step's
-    entity pass; `csr_ready`: this batch is the previous call's next_batch and
-    `workspace` its next_workspace.  Bit-identical to train_step_grads."""
-    if mode not in ("head-batch", "tail-batch"):
-        raise ValueError("Training batch mode %s not supported" % mode)
-    pos, neg = _idx(pos, dev), _idx(neg, dev)
-    w = sub_w.to(dev, dtype=torch.float32, non_blocking=True).contiguous().view(-1)
-    B, n = neg.shape
-    st = state(dev)
-    lib = _lib.load()
-    npos = nneg = None
-    if next_batch is not None:
-        npos, nneg = next_batch
-        if tuple(npos.shape) != (B, 3) or tuple(nneg.shape) != (B, n) or npos.dtype != torch.int64 \
-                or nneg.dtype != torch.int64 or not (npos.is_contiguous() and nneg.is_contiguous()):
-            raise ValueError("next_batch: contiguous int64 tensors of this batch's shapes")
-    _lib.check(lib.kge_train_step_ahead(
-        desc, _lib.MODE_IDS[mode], pos.data_ptr(), neg.data_ptr(), B, n, w.data_ptr(), _ptr(weight_sum_dev),
-        int(bool(uni_weight)), int(uni_batch), int(bool(adversarial)), float(temperature), float(regularization),
-        adam, grad_entity.data_ptr(), grad_relation.data_ptr(), _ptr(grad_modulus), losses.data_ptr(),
-        workspace.data_ptr(), workspace.numel(), st.err.data_ptr(), _stream(dev), int(bool(csr_ready)),
-        _ptr(npos), _ptr(nneg), _ptr(next_workspace), 0 if next_workspace is None else next_workspace.numel()),
-        "kge_train_step_ahead")
-
-
 def _train_ws(desc: _lib.ModelDesc, B: int, n: int, dev) -> torch.Tensor:
     lib = _lib.load()
     key = (desc.entity_dim, desc.relation_dim, desc.nentity, desc.nrelation, B, n)

@@ -224,32 +224,3 @@ def test_filter_device_table_matches_filter_csr():
             got = set(vals[tab[key]:tab[key + 1]].tolist())
             want = set(ids[off[i]:off[i + 1]].tolist()) | {hh if mode == "head-batch" else tt}
             assert got == want, (mode, i)
-
-
-def test_lookahead_batches_kept_per_iterator():
-    """train_step's CSR look-ahead draws one batch early (KGEModel._draw /
-    _take): a batch drawn from one iterator waits for that iterator's next
-    step, so switching iterators and switching the look-ahead off keep every
-    iterator's batches in order, none lost or repeated (host logic only)."""
-    m = KGEModel("TransE", 10, 2, 4, 12.0)
-    cpu = torch.device("cpu")
-
-    def batches(tag, k):
-        return iter([(torch.full((2, 3), tag * 10 + i), torch.full((2, 4), tag * 10 + i), torch.ones(2),
-                      "tail-batch") for i in range(k)])
-
-    a, b = batches(1, 4), batches(2, 3)
-    seen = []
-    # as the look-ahead step does: take this step's batch, then draw the next one and park it
-    for it in (a, a, b, a, b):
-        cur = m._take(it, cpu)
-        seen.append(int(cur[0][0, 0]))
-        nxt = m._draw(it, cpu)
-        if nxt is not None:
-            m._pending[id(it)] = (it, nxt)
-    # a step without the look-ahead takes the parked batch first
-    seen.append(int(m._take(b, cpu)[0][0, 0]))
-    seen.append(int(m._take(a, cpu)[0][0, 0]))
-    assert seen == [10, 11, 20, 12, 21, 22, 13]
-    with pytest.raises(StopIteration):
-        m._take(b, cpu)

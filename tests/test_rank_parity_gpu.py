@@ -396,9 +396,9 @@ def test_device_sinf_within_declared_floats():
         assert int(out.item()) <= bound, (rng, int(out.item()))
 
 
-@pytest.mark.parametrize("name", ["TransE", "pRotatE"])
+@pytest.mark.parametrize("name", ["TransE"])
 def test_tile_staging_switch_same_ranks(name, monkeypatch):
-    """The register tile's round-6 staging for TransE / pRotatE (queries
+    """The register tile's round-6 staging for TransE (queries
     pre-splatted, padded k-rows, pipelined LDS reads) and round 5's
     (KGE_TILE_SPL=0, diagnostic) give the same ranks, ties and listed counts —
     the same arithmetic in the same order."""
