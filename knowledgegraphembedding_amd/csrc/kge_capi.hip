@@ -991,7 +991,7 @@ RankWs carve_rank(void* ws, const kge_model_desc* m, int64_t nq, size_t* bytes) 
   // the entity table's own buffers first, at offsets independent of nq, so a
   // later call on the same workspace can reuse them (KGE_RANK_REUSE_TABLE)
   w.tag = c.take<int64_t>(12);
-  w.stats = c.take<float>(2 + 2 * TS_BLOCKS);  // [max ‖e‖, max |x|, per-block partials]
+  w.stats = c.take<float>(TS_NSTAT * (1 + TS_BLOCKS));  // [the TS_NSTAT maxima, per-block partials]
   // split-bf16 operands: only where the split tile can run (rank_path's x_ok)
   const bool xs = rank_path(m, RP_MFMA) == RP_MFMA;
   w.es = c.take<uint16_t>(xs ? xsplit_elems(m->nentity, m->entity_dim) : 0);
@@ -1141,19 +1141,14 @@ int rank_impl(const kge_model_desc* m, int32_t mode, const int64_t* queries, int
                              (int64_t)(uintptr_t)m->entity_embedding};
   ra.ltag = w.tag ? w.tag + 8 : nullptr;
   for (int k = 0; k < 3; ++k) ra.ltag_v[k] = ltag_v[k];
-  // the split-bf16 tile's error bound in units of u·‖q‖·max‖e‖ (kge_rank_mfma.hip): splitting
-  // residuals and the final add 513.2, the dropped lo·lo products 256·(1 + 2^-8)^2 = 258.1, the
-  // slab's three chained MFMAs 97.6, the running sum 1.02·nslab
+  // the split-bf16 tile's arithmetic error in units of u·‖q‖·max‖e‖ (kge_rank_mfma.hip): the
+  // final add 1.2, the slab's three chained MFMAs 97.6, the running sum 1.02·nslab; the
+  // split's own error is added per query from the pieces' norms (k_rank_window)
   const int64_t xns = xsplit_nslab(m->entity_dim);
-  ra.fast_u = (rp != RP_MFMA) ? 0.f : (float)(513.2 + 258.1 + 97.6 + 1.02 * xns);
-  auto ref_at = [&](int d) {
-    RefArgs x = ra;
-    const int64_t o = d * nq;
-    x.q += o * Le; x.qref += o * Le; x.true_id += o; x.s_true += o; x.sref_true += o; x.s_true_w += o;
-    x.delta += o; x.ucnt += o; x.ulist += o * RANK_CAP; x.fbits += o * W;
-    x.gt += o; x.eq += o; x.gtx += o; x.eqx += o; x.sref_hi += o; x.done += o;
-    return x;
-  };
+  ra.fast_u = (rp != RP_MFMA) ? 0.f : (float)(98.8 + 1.02 * xns);
+  // a refinement stage: both directions' queries in one launch when both
+  // (each block wholly in one direction, kge_kernels.inc ref_dir)
+  auto ref_stage = [&](int stage_) -> int { return launch_status(ops.rank_ref(both ? BOTH_DIRS : mode, stage_, ra, s)); };
   // one launch per direction of a mode-dependent stage (one direction unless both)
   auto per_dir = [&](auto&& launch) -> int {
     for (int d = 0; d < ndir; ++d) {
@@ -1195,23 +1190,40 @@ int rank_impl(const kge_model_desc* m, int32_t mode, const int64_t* queries, int
                                        need_stats ? 1 : 0, rp == RP_MFMA ? 1 : (prot_tile ? 2 : 0),
                                        prot_tile ? kbits : 0, ts));
     if (st) return st;
-    if (need_stats) {
-      st = launch_status(launch_table_stats(m->entity_embedding, m->nentity, m->entity_dim, w.stats, ts, w.tag + 5));
+    if (rp == RP_MFMA && need_stats) {  // (DistMult, ComplEx) one read of the table for both
+      st = launch_status(launch_split_stats(m->entity_embedding, m->nentity, m->entity_dim, w.es, w.stats, ts,
+                                            w.tag + 5, w.tag + 6));
       if (st) return st;
-    }
-    if (rp == RP_MFMA) {
-      st = launch_status(launch_split_bf16(m->entity_embedding, m->nentity, m->entity_dim, w.es, ts, w.tag + 6));
-      if (st) return st;
+    } else {
+      if (need_stats) {
+        st = launch_status(launch_table_stats(m->entity_embedding, m->nentity, m->entity_dim, w.stats, ts, w.tag + 5));
+        if (st) return st;
+      }
+      if (rp == RP_MFMA) {
+        st = launch_status(launch_split_bf16(m->entity_embedding, m->nentity, m->entity_dim, w.es, ts, w.tag + 6));
+        if (st) return st;
+      }
     }
     if (prot_tile) {
       st = launch_status(launch_prot_phase(m->entity_embedding, m->nentity, K, kappa, 1, w.eph, ts, w.tag + 6));
       if (st) return st;
     }
     if (rsd) hipEventRecord(rsd->rk_join, ts);
-    st = per_dir([&](int d, int md) { return launch_status(ops.rank(md, geo.vec, geo.ns, rank_at(d), s)); });
+    if (both && geo.ns != 0) {  // both directions' q in one launch (rows ≤ 2048 floats)
+      RankArgs x = a;
+      x.both_dirs = 1;
+      st = launch_status(ops.rank(KGE_HEAD_BATCH, geo.vec, geo.ns, x, s));
+    } else {
+      st = per_dir([&](int d, int md) { return launch_status(ops.rank(md, geo.vec, geo.ns, rank_at(d), s)); });
+    }
     if (st) return st;
-    // 2. excluded candidates (filtered ids + the true id) as a bitmap
-    st = per_dir([&](int d, int md) {
+    // 2. excluded candidates (filtered ids + the true id) as a bitmap (both
+    // directions in one launch where the row fits LDS)
+    st = both ? launch_filter_bits_both(queries, ftab ? 1 : 0, foff[0], fids[0], foff[1], fids[1], w.true_id, nq,
+                                        m->nentity, m->nrelation, w.bits, err_flag, s)
+              : -1;
+    if (st > 0) return launch_status(st);
+    if (st < 0) st = per_dir([&](int d, int md) {
       const int64_t o = d * nq;
       if (ftab)
         return launch_status(launch_filter_bits_tab(queries, md == KGE_HEAD_BATCH ? 1 : 0, foff[d], fids[d],
@@ -1264,10 +1276,10 @@ int rank_impl(const kge_model_desc* m, int32_t mode, const int64_t* queries, int
     if (st) return st;
     // 4. near-tie windows and the reference-order q
     ra.true_exact = true_ref ? 1 : 0;
-    st = per_dir([&](int d, int md) { return launch_status(ops.rank_ref(md, 0, ref_at(d), s)); });
+    st = ref_stage(0);
     if (st) return st;
     if (true_ref) {
-      st = per_dir([&](int d, int md) { return launch_status(ops.rank_ref(md, 4, ref_at(d), s)); });
+      st = ref_stage(4);
       if (st) return st;
     }
     // 5. fast counting pass: clear cases counted, near-ties listed (the MFMA
@@ -1314,10 +1326,10 @@ int rank_impl(const kge_model_desc* m, int32_t mode, const int64_t* queries, int
   }
   // 6. refinement in the reference's operation order; exact rescan on overflow
   // (RS_FINISH: overflowed pRotatE windows were ranked by the list stage)
-  st = per_dir([&](int d, int md) { return launch_status(ops.rank_ref(md, 1, ref_at(d), s)); });
+  st = ref_stage(1);
   if (st) return st;
   if (stage != RS_FINISH) {
-    st = per_dir([&](int d, int md) { return launch_status(ops.rank_ref(md, 2, ref_at(d), s)); });
+    st = ref_stage(2);
     if (st) return st;
   }
   st = launch_status(launch_rank_emit(ea, s));

@@ -35,9 +35,13 @@ int launch_split_bf16(const float* src, int64_t rows, int K, uint16_t* dst, hipS
 int launch_rank_mfma_x(int gather, const uint16_t* qs, const uint16_t* es, int64_t nq, int64_t E, int K,
                        const int64_t* true_id, float* s_true, const uint32_t* bits, int32_t* gt, const RankWin& win,
                        hipStream_t s);
-constexpr int TS_BLOCKS = 1024;  // k_table_stats grid bound: stats holds 2 + 2·TS_BLOCKS floats
+constexpr int TS_BLOCKS = 2048;  // k_table_stats / k_split_stats grid bound
+constexpr int TS_NSTAT = 4;      // max ‖e‖, max |x|, max ‖r_e‖, max ‖lo_e‖: stats holds TS_NSTAT·(1 + TS_BLOCKS) floats
 int launch_table_stats(const float* ent, int64_t E, int Le, float* stats, hipStream_t s,
                        const int64_t* skip = nullptr);
+// the entity table's split (launch_split_bf16) and statistics (launch_table_stats) in one read
+int launch_split_stats(const float* ent, int64_t E, int K, uint16_t* dst, float* stats, hipStream_t s,
+                       const int64_t* skip_stats, const int64_t* skip_split);
 // the ranking workspace's table tag (KGE_RANK_REUSE_TABLE; kge_rank_mfma.hip k_rank_tag)
 int launch_rank_tag(int64_t* tag, const float* ent, int64_t E, int Le, int reuse, int need_stats, int split_kind,
                     int64_t split_param, hipStream_t s);
@@ -49,6 +53,11 @@ int launch_prot_phase(const float* src, int64_t rows, int K, float kappa, int en
 int launch_filter_bits_tab(const int64_t* queries, int head, const int64_t* tab, const int64_t* vals,
                            const int64_t* true_id, int64_t nq, int64_t E, int64_t R, uint32_t* bits, int32_t* err,
                            hipStream_t s);
+// both directions in one launch (blocks nq.. tail-batch's): tab != 0 → off_* are the
+// dense key tables, else per-query list offsets; -1 when the rows are too wide (per direction then)
+int launch_filter_bits_both(const int64_t* queries, int tab, const int64_t* off_h, const int64_t* ids_h,
+                            const int64_t* off_t, const int64_t* ids_t, const int64_t* true_id, int64_t nq,
+                            int64_t E, int64_t R, uint32_t* bits, int32_t* err, hipStream_t s);
 int launch_filter_bits(const int64_t* filt_off, const int64_t* filt_ids, const int64_t* true_id, int64_t nq,
                        int64_t E, uint32_t* bits, int32_t* err, hipStream_t s);
 struct EmitArgs {

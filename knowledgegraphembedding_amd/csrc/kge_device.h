@@ -32,6 +32,8 @@ namespace kge {
 
 enum Model : int { TRANSE = 0, DISTMULT = 1, COMPLEX = 2, ROTATE = 3, PROTATE = 4 };
 enum Mode : int { SINGLE = 0, HEAD_BATCH = 1, TAIL_BATCH = 2 };
+// (ranking refinement launches only: both directions' queries in one grid)
+constexpr int BOTH_DIRS = 3;
 
 template <int M>
 struct Traits {
@@ -218,6 +220,24 @@ __device__ __forceinline__ float wave_sum(float x) {
   x = x + dppf<0x141>(x);  // row_half_mirror
   x = x + dppf<0x140>(x);  // row_mirror
   return (readlanef(x, 0) + readlanef(x, 16)) + (readlanef(x, 32) + readlanef(x, 48));
+}
+
+// bf16 bits of x, round-to-nearest-even (NaN → quiet NaN): the split-bf16
+// ranking tile's operand pieces (kge_rank_mfma.hip)
+__device__ __forceinline__ uint32_t bf16_rne(float x) {
+  const uint32_t b = __float_as_uint(x);
+  if (x != x) return 0x7FC0u;
+  return (b + 0x7FFFu + ((b >> 16) & 1u)) >> 16;
+}
+// x = hi + lo + r exactly, hi = bf16(x), lo = bf16(x − hi) (both differences
+// are exact in fp32): the lo piece and the residual r, scaled by 2^8 and 2^16
+// (exact) so their squares stay normal wherever x's do — the split tile's
+// data-dependent error bound sums them (k_split_stats, k_rank_window)
+__device__ __forceinline__ void bf16_split_scaled(float x, float& lo8, float& r16) {
+  const float r1 = x - __uint_as_float(bf16_rne(x) << 16);
+  const float lo = __uint_as_float(bf16_rne(r1) << 16);
+  lo8 = lo * 256.f;
+  r16 = (r1 - lo) * 65536.f;
 }
 
 // Hardware square root / reciprocal (v_sqrt_f32 / v_rcp_f32, ~1 ulp) for the

@@ -212,6 +212,8 @@ struct RankArgs {
   int32_t* err;
   int prep_only;        // launch k_rank_prep only (the MFMA / tile paths count on their own)
   int zero_counts;      // k_rank_prep zeroes gt and the five counters after it (eq, gtx, eqx, ucnt, done)
+  int both_dirs;        // (prep_only) both directions in one launch: queries [nq, 3] shared, per-query
+                        // arrays of 2·nq (head-batch's first); not for wide rows
   int64_t cstride;      // distance between those counter arrays (the workspace's query count: nq, or 2·nq
                         // when both directions share one workspace and gt points into it)
   const float* trig;    // RotatE: [R, 2, Lr] reference cos | sin of the phases, or null

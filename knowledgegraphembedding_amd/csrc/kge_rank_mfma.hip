@@ -304,16 +304,29 @@ __global__ __launch_bounds__(256) void k_filter_bits_tab(const int64_t* __restri
 // ids' bits there (LDS atomics), and writes the whole row out with coalesced
 // stores — no separate memset of the [nq, W] bitmap and no global atomics.
 // `tab` non-null: the filter index's dense key → start table (k_filter_bits_tab's
-// lookup, `head` picks the key); else per-query lists off / ids.
+// lookup, `head` picks the key); else per-query lists off / ids.  A grid of
+// 2·nq blocks ranks both directions: blocks nq.. are tail-batch's, with the
+// tail table / lists (tab1 / off1, ids1), the same queries and the second half
+// of true_id and bits.
 __global__ __launch_bounds__(256) void k_filter_bits_lds(const int64_t* __restrict__ queries, int head,
                                                          const int64_t* __restrict__ tab,
                                                          const int64_t* __restrict__ off,
                                                          const int64_t* __restrict__ ids,
                                                          const int64_t* __restrict__ true_id, int64_t nq, int64_t E,
                                                          int64_t R, int W, uint32_t* __restrict__ bits,
-                                                         int32_t* err) {
+                                                         int32_t* err, const int64_t* __restrict__ tab1,
+                                                         const int64_t* __restrict__ off1,
+                                                         const int64_t* __restrict__ ids1) {
   extern __shared__ uint32_t fb_row[];
-  const int64_t q = blockIdx.x;
+  const int64_t q = blockIdx.x;  // (index into true_id and bits)
+  const bool d1 = q >= nq;
+  const int64_t ql = d1 ? q - nq : q;  // (index into queries and the lists)
+  if (d1) {
+    tab = tab1;
+    off = off1;
+    ids = ids1;
+    head = 0;
+  }
   const int tid = threadIdx.x;
   for (int k = tid; k < W; k += 256) fb_row[k] = 0u;
   __syncthreads();
@@ -321,15 +334,15 @@ __global__ __launch_bounds__(256) void k_filter_bits_lds(const int64_t* __restri
   if (tid == 0 && t >= 0 && t < E) atomicOr(&fb_row[t >> 5], 1u << (t & 31));
   int64_t b = 0, e_ = 0;
   if (tab) {
-    const int64_t h = queries[q * 3], r = queries[q * 3 + 1], tl = queries[q * 3 + 2];
+    const int64_t h = queries[ql * 3], r = queries[ql * 3 + 1], tl = queries[ql * 3 + 2];
     if (h >= 0 && h < E && tl >= 0 && tl < E && r >= 0 && r < R) {  // (k_rank_prep flags bad ids)
       const int64_t key = head ? r * E + tl : h * R + r;
       b = tab[key];
       e_ = tab[key + 1];
     }
   } else {
-    b = off[q];
-    e_ = off[q + 1];
+    b = off[ql];
+    e_ = off[ql + 1];
   }
   for (int64_t p = b + tid; p < e_; p += 256) {
     const int64_t e = ids[p];
@@ -381,13 +394,18 @@ __global__ __launch_bounds__(256) void k_rank_emit(EmitArgs a) {
 // are exact in fp32); the chain's result joins an fp32 running sum (one
 // rounding per slab); e_lo·q_lo is never computed.  Error per score against
 // the exact Σ e_k q_k, u = 2^-24, P = Σ|q_k||e_k| ≤ ‖q‖‖e‖:
-//   splitting residuals      2·2^-16·P (+ the final add's 1.01·u·P) → 513.2·u·P
-//   the dropped lo·lo        2^-16 (1 + 2^-8)^2·P                   → 258.1·u·P
+//   the split itself         Σ|q||r_e| + Σ|r_q||e| + Σ|r_q||r_e| + Σ|q_lo||e_lo|
+//                            ≤ ‖q‖‖r_e‖ + ‖r_q‖‖e‖ + ‖r_q‖‖r_e‖ + ‖q_lo‖‖e_lo‖, from the
+//                            pieces' actual norms (round 6; k_split_stats / k_table_stats
+//                            keep the table's maxima, k_rank_window computes q's) — the
+//                            worst case 2·2^-16·P + 2^-16 (1 + 2^-8)^2·P = 770·u·P of
+//                            rounds 4-5 is ≈ 126·u·P on uniform tables
+//   the final add            1.2·u·P
 //   the three chained MFMAs  ≤ 32·u each on partial sums ≤ (1 + 2^-8)^2 (1 + 2^-7)·P_slab
 //                            (2u per internal add, any order)      →  97.6·u·P
 //   the running sum          1.02·nslab·u·P
-// → fast_u = (868.9 + 1.02·nslab)·u·P (kge_capi.hip rank_impl, RefArgs.fast_u;
-// the window k_rank_window sizes from it), against the fp32 tile's K·u.
+// → fast_u = (98.8 + 1.02·nslab)·u·P plus the split term (kge_capi.hip rank_impl,
+// RefArgs.fast_u; the window k_rank_window sizes from both), against the fp32 tile's K·u.
 //
 // Operands are split once per call into a tile-linear layout
 // [row block of 128][16-k slab][hi | lo][128 rows][16 k] bf16 (k_split_bf16),
@@ -404,12 +422,6 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 constexpr int XS_BK = 16;                   // k per slab = one 32x32x16 MFMA step
 constexpr int XS_PIECE = 128 * XS_BK;       // bf16 per (row block, slab, hi|lo) = 4 KB
 constexpr uint32_t XS_OOB = 0x7FFFFFF0u;
-
-__device__ __forceinline__ uint32_t bf16_rne(float x) {
-  const uint32_t b = __float_as_uint(x);
-  if (x != x) return 0x7FC0u;
-  return (b + 0x7FFFu + ((b >> 16) & 1u)) >> 16;
-}
 
 // dst[(rb·nslab + s)·2 + piece][rr][kk] for rows < rows, k < K (zeros elsewhere).
 // A wave takes 8 rows × 64 k: lane (r8, g8) = (lane >> 3, lane & 7) converts
@@ -450,6 +462,100 @@ __global__ __launch_bounds__(256) void k_split_bf16(const float* __restrict__ sr
                 ((kg & 1) ^ (int)((row >> 3) & 1)) * 8;
   *reinterpret_cast<uint4*>(o) = vh;
   *reinterpret_cast<uint4*>(o + XS_PIECE) = vl;
+}
+
+// The entity table's split and its statistics (k_table_stats' four maxima,
+// TS_NSTAT) in one read of the table: a wave takes 8 whole rows (lane
+// (r8, g8) converts floats 64·c + 8·g8 … of row r8 for every 64-k chunk c, the
+// same per-slab stores as k_split_bf16), its 8 lanes per row reduce the row's
+// sums, and each block writes its partial maxima to stats[4 + 4·block] for
+// k_stats_reduce.  Row groups are strided
+// over ≤ TS_BLOCKS blocks.  (The separate statistics pass re-read the 84 MB
+// wn18rr table: 19 µs of a 1.07 ms DistMult evaluation.)
+// one row's contribution to the TS_NSTAT maxima from its Σx², max |x| and
+// the Σ of its scaled split pieces (bf16_split_scaled: lo·2^8, r·2^16); each
+// norm × mg = 1.0001 + Le·3.1e-8 for its fp32 sum of ≤ Le terms in any order
+// (√ of a γ_Le-relative sum: ≤ γ_Le / 2 + u)
+__device__ __forceinline__ void table_stats_row(float (&bs)[TS_NSTAT], float s2, float mx, float sl, float sr,
+                                                float mg) {
+  bs[0] = fmaxf(bs[0], sqrtf(s2) * mg);
+  bs[1] = fmaxf(bs[1], mx);
+  bs[2] = fmaxf(bs[2], sqrtf(sr) * mg * 0x1p-16f);
+  bs[3] = fmaxf(bs[3], sqrtf(sl) * mg * 0x1p-8f);
+}
+
+__global__ __launch_bounds__(256) void k_split_stats(const float* __restrict__ src, int64_t rows, int K, int nslab,
+                                                     int64_t nrb, uint16_t* __restrict__ dst, float* stats,
+                                                     const int64_t* skip_stats, const int64_t* skip_split) {
+  const bool do_stats = !(skip_stats && *skip_stats), do_split = !(skip_split && *skip_split);
+  if (!do_stats && !do_split) return;  // the workspace holds both for this table (k_rank_tag)
+  __shared__ float red[TS_NSTAT][4];
+  const int lane = threadIdx.x & 63, w = wave_id();
+  const int r8 = lane >> 3, g8 = lane & 7;
+  const int nc = (nslab * XS_BK + 63) / 64;  // 64-k chunks per row
+  const bool vec = ((K & 3) == 0) && ((((uintptr_t)src) & 15) == 0);
+  float bs[TS_NSTAT] = {0.f, 0.f, 0.f, 0.f};
+  for (int64_t rg = (int64_t)blockIdx.x * 4 + w; rg < nrb * 16; rg += (int64_t)gridDim.x * 4) {
+    const int64_t row = rg * 8 + r8;
+    const int64_t rb = row >> 7;
+    float s2 = 0.f, mx = 0.f, sr = 0.f, sl = 0.f;
+    for (int c = 0; c < nc; ++c) {
+      const int kg = c * 8 + g8;  // 8-k group
+      if (kg >= nslab * 2) break;
+      const int k0 = kg * 8;
+      float x[8];
+      const float* p = src + row * K + k0;
+      if (row < rows && k0 + 8 <= K && vec) {
+        const float4 a = reinterpret_cast<const float4*>(p)[0], b = reinterpret_cast<const float4*>(p)[1];
+        x[0] = a.x; x[1] = a.y; x[2] = a.z; x[3] = a.w; x[4] = b.x; x[5] = b.y; x[6] = b.z; x[7] = b.w;
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) x[j] = (row < rows && k0 + j < K) ? p[j] : 0.f;
+      }
+      uint32_t hi[8], lo[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        s2 += x[j] * x[j];
+        mx = fmaxf(mx, fabsf(x[j]));
+        hi[j] = bf16_rne(x[j]);
+        lo[j] = bf16_rne(x[j] - __uint_as_float(hi[j] << 16));  // exact difference
+        float l8, r16;
+        bf16_split_scaled(x[j], l8, r16);
+        sl += l8 * l8;
+        sr += r16 * r16;
+      }
+      if (do_split) {
+        const uint4 vh = {hi[0] | (hi[1] << 16), hi[2] | (hi[3] << 16), hi[4] | (hi[5] << 16), hi[6] | (hi[7] << 16)};
+        const uint4 vl = {lo[0] | (lo[1] << 16), lo[2] | (lo[3] << 16), lo[4] | (lo[5] << 16), lo[6] | (lo[7] << 16)};
+        uint16_t* o = dst + ((rb * nslab + (kg >> 1)) * 2) * XS_PIECE + (row & 127) * XS_BK +
+                      ((kg & 1) ^ (int)((row >> 3) & 1)) * 8;
+        *reinterpret_cast<uint4*>(o) = vh;
+        *reinterpret_cast<uint4*>(o + XS_PIECE) = vl;
+      }
+    }
+    // the row's 8 lanes: the sums (any order: the norms' 1.0001 covers γ_K) and max |x|
+#pragma unroll
+    for (int o = 1; o < 8; o <<= 1) {
+      s2 += __shfl_xor(s2, o);
+      sl += __shfl_xor(sl, o);
+      sr += __shfl_xor(sr, o);
+      mx = fmaxf(mx, __shfl_xor(mx, o));
+    }
+    table_stats_row(bs, s2, mx, sl, sr, 1.0001f + (float)K * 3.1e-8f);
+  }
+  if (!do_stats) return;
+#pragma unroll
+  for (int o = 8; o < 64; o <<= 1)
+#pragma unroll
+    for (int i = 0; i < TS_NSTAT; ++i) bs[i] = fmaxf(bs[i], __shfl_xor(bs[i], o));
+  if (lane == 0)
+#pragma unroll
+    for (int i = 0; i < TS_NSTAT; ++i) red[i][w] = bs[i];
+  __syncthreads();
+  if (threadIdx.x < TS_NSTAT) {
+    const int i = threadIdx.x;
+    stats[TS_NSTAT + TS_NSTAT * blockIdx.x + i] = fmaxf(fmaxf(red[i][0], red[i][1]), fmaxf(red[i][2], red[i][3]));
+  }
 }
 
 struct XArgs {
@@ -756,7 +862,7 @@ int launch_filter_bits(const int64_t* filt_off, const int64_t* filt_ids, const i
   if (nq > 65535) return -1;
   if (W <= FB_LDS_WORDS) {
     hipLaunchKernelGGL(k_filter_bits_lds, dim3((unsigned)nq), dim3(256), (size_t)W * 4, s, nullptr, 0, nullptr,
-                       filt_off, filt_ids, true_id, nq, E, (int64_t)0, (int)W, bits, err);
+                       filt_off, filt_ids, true_id, nq, E, (int64_t)0, (int)W, bits, err, nullptr, nullptr, nullptr);
     return (int)hipGetLastError();
   }
   hipError_t he = hipMemsetAsync(bits, 0, (size_t)nq * W * 4, s);
@@ -772,13 +878,27 @@ int launch_filter_bits_tab(const int64_t* queries, int head, const int64_t* tab,
   const int64_t W = (E + 31) / 32;
   if (W <= FB_LDS_WORDS && nq <= 0x7fffffff) {
     hipLaunchKernelGGL(k_filter_bits_lds, dim3((unsigned)nq), dim3(256), (size_t)W * 4, s, queries, head, tab,
-                       nullptr, vals, true_id, nq, E, R, (int)W, bits, err);
+                       nullptr, vals, true_id, nq, E, R, (int)W, bits, err, nullptr, nullptr, nullptr);
     return (int)hipGetLastError();
   }
   hipError_t he = hipMemsetAsync(bits, 0, (size_t)nq * W * 4, s);
   if (he != hipSuccess) return (int)he;
   hipLaunchKernelGGL(k_filter_bits_tab, dim3((unsigned)((nq + 3) / 4)), dim3(256), 0, s, queries, head, tab, vals,
                      true_id, nq, E, R, W, bits, err);
+  return (int)hipGetLastError();
+}
+
+int launch_filter_bits_both(const int64_t* queries, int tab, const int64_t* off_h, const int64_t* ids_h,
+                            const int64_t* off_t, const int64_t* ids_t, const int64_t* true_id, int64_t nq,
+                            int64_t E, int64_t R, uint32_t* bits, int32_t* err, hipStream_t s) {
+  const int64_t W = (E + 31) / 32;
+  if (W > FB_LDS_WORDS || 2 * nq > 0x7fffffff) return -1;  // (the caller runs a launch per direction)
+  if (tab)
+    hipLaunchKernelGGL(k_filter_bits_lds, dim3((unsigned)(2 * nq)), dim3(256), (size_t)W * 4, s, queries, 1, off_h,
+                       nullptr, ids_h, true_id, nq, E, R, (int)W, bits, err, off_t, nullptr, ids_t);
+  else
+    hipLaunchKernelGGL(k_filter_bits_lds, dim3((unsigned)(2 * nq)), dim3(256), (size_t)W * 4, s, queries, 0,
+                       nullptr, off_h, ids_h, true_id, nq, E, R, (int)W, bits, err, nullptr, off_t, ids_t);
   return (int)hipGetLastError();
 }
 
@@ -914,28 +1034,38 @@ int launch_rank_mfma_x(int gather, const uint16_t* qs, const uint16_t* es, int64
   return (int)hipGetLastError();
 }
 
-// Entity-table statistics for the ranking windows: stats[0] = max row L2
-// norm, stats[1] = max |x|.  Each wave takes TS_ROWS rows at a time with their
+// Entity-table statistics for the ranking windows (TS_NSTAT maxima over the
+// rows): stats[0] = max row L2 norm ‖e‖, stats[1] = max |x|, stats[2] = max
+// ‖r_e‖ and stats[3] = max ‖lo_e‖ of the rows' bf16 splits (e = hi + lo + r;
+// the split tile's error bound, k_rank_window).  Each wave takes TS_ROWS rows at a time with their
 // loads interleaved (TS_ROWS float4s in flight per lane; one row per wave at a
 // time left the pass latency-bound: 0.24 ms for wn18rr's 40,943 × 500 table,
-// r02), rows strided over a bounded grid; each block writes its two partial
-// maxima to stats[2 + 2·block] and one small block reduces them (the
+// r02), rows strided over a bounded grid; each block writes its partial
+// maxima to stats[4 + 4·block] and one small block reduces them (the
 // per-block atomics on the same two words serialised at ≈11 ns each: 23 µs of
-// the 35 µs pass; per row, 0.93 ms).  stats needs 2 + 2·TS_BLOCKS floats.
+// the 35 µs pass; per row, 0.93 ms).  stats needs TS_NSTAT·(1 + TS_BLOCKS) floats.
 constexpr int TS_ROWS = 4;
 __global__ __launch_bounds__(256) void k_table_stats(const float* __restrict__ ent, int64_t E, int Le,
                                                      float* stats, const int64_t* skip) {
   if (skip && *skip) return;  // still valid in the workspace (k_rank_tag)
-  __shared__ float red[2][4];
+  __shared__ float red[TS_NSTAT][4];
   const int lane = threadIdx.x & 63, w = wave_id();
   const bool vec4 = (Le & 3) == 0 && (((uintptr_t)ent) & 15) == 0;
   const int nk = vec4 ? Le / 4 : Le;
-  float bn = 0.f, bm = 0.f;
+  float bs[TS_NSTAT] = {0.f, 0.f, 0.f, 0.f};
   const int64_t stride = (int64_t)gridDim.x * 4 * TS_ROWS;
   for (int64_t e0 = ((int64_t)blockIdx.x * 4 + w) * TS_ROWS; e0 < E; e0 += stride) {
-    float s2[TS_ROWS], mx[TS_ROWS];
+    float s2[TS_ROWS], mx[TS_ROWS], sl[TS_ROWS], sr[TS_ROWS];
 #pragma unroll
-    for (int r = 0; r < TS_ROWS; ++r) s2[r] = mx[r] = 0.f;
+    for (int r = 0; r < TS_ROWS; ++r) s2[r] = mx[r] = sl[r] = sr[r] = 0.f;
+    auto acc = [&](int r, float v) {
+      float l8, r16;
+      bf16_split_scaled(v, l8, r16);
+      s2[r] += v * v;
+      sl[r] += l8 * l8;
+      sr[r] += r16 * r16;
+      mx[r] = fmaxf(mx[r], fabsf(v));
+    };
     for (int k = lane; k < nk; k += 64) {
 #pragma unroll
       for (int r = 0; r < TS_ROWS; ++r) {
@@ -943,53 +1073,63 @@ __global__ __launch_bounds__(256) void k_table_stats(const float* __restrict__ e
         const float* row = ent + (e0 + r) * Le;
         if (vec4) {
           const float4 v = reinterpret_cast<const float4*>(row)[k];
-          s2[r] += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
-          mx[r] = fmaxf(mx[r], fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+          acc(r, v.x); acc(r, v.y); acc(r, v.z); acc(r, v.w);
         } else {
-          const float v = row[k];
-          s2[r] += v * v;
-          mx[r] = fmaxf(mx[r], fabsf(v));
+          acc(r, row[k]);
         }
       }
     }
 #pragma unroll
     for (int r = 0; r < TS_ROWS; ++r) {
-      const float t2 = wave_sum(s2[r]);
       float m = mx[r];
 #pragma unroll
       for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
-      bn = fmaxf(bn, sqrtf(t2) * 1.0001f);
-      bm = fmaxf(bm, m);
+      table_stats_row(bs, wave_sum(s2[r]), m, wave_sum(sl[r]), wave_sum(sr[r]), 1.0001f + (float)Le * 3.1e-8f);
     }
   }
-  if (lane == 0) { red[0][w] = bn; red[1][w] = bm; }
+  if (lane == 0)
+#pragma unroll
+    for (int i = 0; i < TS_NSTAT; ++i) red[i][w] = bs[i];
   __syncthreads();
-  if (threadIdx.x == 0) {
-    stats[2 + 2 * blockIdx.x] = fmaxf(fmaxf(red[0][0], red[0][1]), fmaxf(red[0][2], red[0][3]));
-    stats[3 + 2 * blockIdx.x] = fmaxf(fmaxf(red[1][0], red[1][1]), fmaxf(red[1][2], red[1][3]));
+  if (threadIdx.x < TS_NSTAT) {
+    const int i = threadIdx.x;
+    stats[TS_NSTAT + TS_NSTAT * blockIdx.x + i] = fmaxf(fmaxf(red[i][0], red[i][1]), fmaxf(red[i][2], red[i][3]));
   }
 }
 
 __global__ __launch_bounds__(256) void k_stats_reduce(float* stats, int nblocks, const int64_t* skip) {
   if (skip && *skip) return;
-  __shared__ float red[2][4];
+  __shared__ float red[TS_NSTAT][4];
   const int lane = threadIdx.x & 63, w = wave_id();
-  float n = 0.f, m = 0.f;
-  for (int b = threadIdx.x; b < nblocks; b += 256) {
-    n = fmaxf(n, stats[2 + 2 * b]);
-    m = fmaxf(m, stats[3 + 2 * b]);
-  }
+  float v[TS_NSTAT] = {0.f, 0.f, 0.f, 0.f};
+  for (int b = threadIdx.x; b < nblocks; b += 256)
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    n = fmaxf(n, __shfl_xor(n, o));
-    m = fmaxf(m, __shfl_xor(m, o));
-  }
-  if (lane == 0) { red[0][w] = n; red[1][w] = m; }
+    for (int i = 0; i < TS_NSTAT; ++i) v[i] = fmaxf(v[i], stats[TS_NSTAT + TS_NSTAT * b + i]);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1)
+#pragma unroll
+    for (int i = 0; i < TS_NSTAT; ++i) v[i] = fmaxf(v[i], __shfl_xor(v[i], o));
+  if (lane == 0)
+#pragma unroll
+    for (int i = 0; i < TS_NSTAT; ++i) red[i][w] = v[i];
   __syncthreads();
-  if (threadIdx.x == 0) {
-    stats[0] = fmaxf(fmaxf(red[0][0], red[0][1]), fmaxf(red[0][2], red[0][3]));
-    stats[1] = fmaxf(fmaxf(red[1][0], red[1][1]), fmaxf(red[1][2], red[1][3]));
+  if (threadIdx.x < TS_NSTAT) {
+    const int i = threadIdx.x;
+    stats[i] = fmaxf(fmaxf(red[i][0], red[i][1]), fmaxf(red[i][2], red[i][3]));
   }
+}
+
+int launch_split_stats(const float* ent, int64_t E, int K, uint16_t* dst, float* stats, hipStream_t s,
+                       const int64_t* skip_stats, const int64_t* skip_split) {
+  const int64_t nrb = (E + 127) / 128, nslab = xsplit_nslab(K);
+  const int64_t want = (nrb * 16 + 3) / 4;  // a wave per 8-row group
+  const int blocks = (int)(want < TS_BLOCKS ? (want > 0 ? want : 1) : TS_BLOCKS);
+  hipLaunchKernelGGL(k_split_stats, dim3((unsigned)blocks), dim3(256), 0, s, ent, E, K, (int)nslab, nrb, dst, stats,
+                     skip_stats, skip_split);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return (int)e;
+  hipLaunchKernelGGL(k_stats_reduce, dim3(1), dim3(256), 0, s, stats, blocks, skip_stats);
+  return (int)hipGetLastError();
 }
 
 int launch_table_stats(const float* ent, int64_t E, int Le, float* stats, hipStream_t s, const int64_t* skip) {
