@@ -101,9 +101,10 @@ typedef struct kge_model_desc {
 /* Library identity: "knowledgegraphembedding_amd <KGE_ABI_VERSION> gfx950".  The
  * version changes with every change of a struct, a signature or a call
  * protocol in this header (0.3: pRotatE's three-call item counts; 0.4:
- * kge_rank_filtered_both, the ranking timer counting directions);
+ * kge_rank_filtered_both, the ranking timer counting directions; 0.5: the
+ * one-step-ahead training CSR entry point of an earlier 0.4 build removed);
  * loaders refuse a library whose version differs from the header they bind. */
-#define KGE_ABI_VERSION "0.4"
+#define KGE_ABI_VERSION "0.5"
 const char *kge_version(void);
 const char *kge_status_string(int status);
 

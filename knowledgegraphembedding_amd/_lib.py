@@ -18,7 +18,7 @@ MODE_IDS = {"single": 0, "head-batch": 1, "tail-batch": 2}
 DEVERR_INDEX = 1
 DEVERR_SAMPLER = 2
 DEVERR_ARG = 4
-ABI_VERSION = "0.4"  # KGE_ABI_VERSION of the include/kge_hip.h this binding mirrors
+ABI_VERSION = "0.5"  # KGE_ABI_VERSION of the include/kge_hip.h this binding mirrors
 RANK_STAGE_LIST = 0x200  # KGE_RANK_STAGE_LIST
 RANK_FILTER_TABLE = 0x400  # KGE_RANK_FILTER_TABLE
 RANK_LIST_CAP = 1024  # KGE_RANK_LIST_CAP

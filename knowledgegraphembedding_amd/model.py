@@ -25,7 +25,7 @@ import torch
 import torch.nn as nn
 
 from . import _lib, ops, torch_ops  # noqa: F401  (torch_ops registers torch.ops.kge.*)
-from .filters import FilterIndex
+from .filters import FilterIndex, triples_array
 
 _MODELS = ['TransE', 'DistMult', 'ComplEx', 'RotatE', 'pRotatE']
 
@@ -514,7 +514,7 @@ class KGEModel(nn.Module):
         # Filtered MRR / MR / HITS@{1,3,10}: head-batch queries, then tail-batch
         # (model.py:349-418); the filter is dataloader.py:134-154's.
         index = FilterIndex(all_true_triples, args.nentity, args.nrelation)
-        triples = np.asarray(test_triples, dtype=np.int64).reshape(-1, 3)
+        triples = triples_array(test_triples)
         desc = model.desc()
         ranks_seq = []  # head-batch queries, then tail-batch, as the reference's logs list
         test_batch_size = max(1, int(args.test_batch_size))

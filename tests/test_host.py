@@ -224,3 +224,24 @@ def test_filter_device_table_matches_filter_csr():
             got = set(vals[tab[key]:tab[key + 1]].tolist())
             want = set(ids[off[i]:off[i + 1]].tolist()) | {hh if mode == "head-batch" else tt}
             assert got == want, (mode, i)
+
+
+def test_filter_device_table_built_by_search_matches_host_table(monkeypatch):
+    """Key spaces above DENSE_KEYS get their start table from a search of
+    every key in the sorted keys on the device (FB15k: 20.1 M keys); it equals
+    the host's tabulated table (run here on the CPU device)."""
+    from knowledgegraphembedding_amd import synth
+    from knowledgegraphembedding_amd.filters import FilterIndex
+    E, R = 300, 17
+    t = np.stack([synth.randint(31, (4000,), E), synth.randint(32, (4000,), R), synth.randint(33, (4000,), E)], 1)
+    index = FilterIndex([tuple(map(int, x)) for x in t], E, R)
+    assert np.array_equal(index._k_hr, FilterIndex(t, E, R)._k_hr)  # list-of-tuples input as the array
+    for mode in ("head-batch", "tail-batch"):
+        host_tab, host_vals = index.device_table(mode, "cpu")
+        monkeypatch.setattr(FilterIndex, "DENSE_KEYS", 16)
+        index.__dict__.pop("_dev_tables", None)
+        tab, vals = index.device_table(mode, "cpu")
+        monkeypatch.setattr(FilterIndex, "DENSE_KEYS", 1 << 22)
+        index.__dict__.pop("_dev_tables", None)
+        assert tab.shape == (E * R + 1,) and tab.dtype == torch.int64
+        assert torch.equal(tab, host_tab) and torch.equal(vals, host_vals), mode

@@ -379,6 +379,15 @@ def test_filter_table_matches_query_lists(name, monkeypatch):
     monkeypatch.setenv("KGE_RANK_FILTER_TABLE", "0")
     (rh2, th2), (rt2, tt2) = m.rank_queries_both(test, index)
     assert np.array_equal(rh2, rh) and np.array_equal(rt2, rt) and np.array_equal(th2, th) and np.array_equal(tt2, tt)
+    # key spaces above DENSE_KEYS: the start table searched on the device (FB15k's path)
+    monkeypatch.delenv("KGE_RANK_FILTER_TABLE")
+    host = [index.device_table(md, DEV) for md in ("head-batch", "tail-batch")]
+    monkeypatch.setattr(FilterIndex, "DENSE_KEYS", 16)
+    index.__dict__.pop("_dev_tables", None)
+    searched = [index.device_table(md, DEV) for md in ("head-batch", "tail-batch")]
+    assert all(torch.equal(a[0], b[0]) and torch.equal(a[1], b[1]) for a, b in zip(host, searched))
+    (rh3, th3), (rt3, tt3) = m.rank_queries_both(test, index)
+    assert np.array_equal(rh3, rh) and np.array_equal(rt3, rt) and np.array_equal(th3, th) and np.array_equal(tt3, tt)
 
 
 def test_device_sinf_within_declared_floats():
