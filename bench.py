@@ -408,7 +408,8 @@ def test_step_section(dev) -> dict:
     KGEModel.test_step(m, test_l[:64], all_true[:4096], args)  # warm-up: first-use state, not timed
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    FilterIndex(all_true, Ef, Rf)
+    FilterIndex(all_true, Ef, Rf, device=dev)  # as test_step builds it (on the GPU)
+    torch.cuda.synchronize()
     t_index = time.perf_counter() - t0
     lib = _lib.load()
     _lib.check(lib.kge_stage_timer(4, None, 0), "kge_stage_timer")

@@ -26,10 +26,41 @@ def triples_array(triples) -> np.ndarray:
 
 
 class FilterIndex:
-    def __init__(self, all_true_triples, nentity: int, nrelation: int):
+    """`device`: the two sorted key orders are built there with torch (unique
+    / sort of the packed keys — on a GPU, test_step's index for an FB15k-size
+    graph in a few ms instead of ≈20 ms of numpy) and the host arrays are
+    made from them only when a host method needs them (filter_csr)."""
+
+    _HOST = ('_k_hr', '_tails', '_k_rt', '_heads')
+
+    def __init__(self, all_true_triples, nentity: int, nrelation: int, device=None):
         t = triples_array(all_true_triples)
         self.nentity = int(nentity)
         self.nrelation = int(nrelation)
+        R, E = self.nrelation, self.nentity
+        self._on = None  # (device, {mode: (sorted keys, ids)}) when built on a GPU
+        if device is not None and R * E * E < 2 ** 62 and len(t):
+            import torch
+            td = torch.from_numpy(t).to(device)
+            hr_t = torch.unique((td[:, 0] * R + td[:, 1]) * E + td[:, 2])  # sorted: set(all_true_triples)
+            k_hr, tails = hr_t // E, hr_t % E
+            h, r = k_hr // R, k_hr % R
+            rt_h = torch.sort((r * E + tails) * E + h).values
+            self._on = (str(device), {'tail-batch': (k_hr, tails), 'head-batch': (rt_h // E, rt_h % E)})
+            return
+        self._build_host(t)
+
+    def __getattr__(self, name):
+        # the host arrays of an index built on the device, made on first use
+        if name in FilterIndex._HOST and self.__dict__.get('_on') is not None:
+            d = self._on[1]
+            (kh, tl), (kr, hd) = d['tail-batch'], d['head-batch']
+            for n, v in zip(FilterIndex._HOST, (kh, tl, kr, hd)):
+                self.__dict__[n] = v.cpu().numpy()
+            return self.__dict__[name]
+        raise AttributeError(name)
+
+    def _build_host(self, t):
         R, E = self.nrelation, self.nentity
         if R * E * E < 2 ** 62:
             # set(all_true_triples) (dataloader.py:125) and both orders as sorts
@@ -87,10 +118,15 @@ class FilterIndex:
         cache = self.__dict__.setdefault('_dev_tables', {})
         k = (mode, str(dev))
         if k not in cache:
-            if n <= self.DENSE_KEYS:
+            import torch
+            if self._on is not None and self._on[0] == str(dev):
+                # built on this device: the table is the search of every key in its sorted keys
+                self._sorted(mode)  # (mode check)
+                cd, vals = self._on[1][mode]
+                cache[k] = (torch.searchsorted(cd, torch.arange(n + 1, dtype=torch.int64, device=dev)), vals)
+            elif n <= self.DENSE_KEYS:
                 cache[k] = self._host_table_on(mode, dev)
             else:
-                import torch
                 cand, vals = self._sorted(mode)
                 cd = torch.from_numpy(np.ascontiguousarray(cand, dtype=np.int64)).to(dev)
                 tab = torch.searchsorted(cd, torch.arange(n + 1, dtype=torch.int64, device=dev))
@@ -98,15 +134,16 @@ class FilterIndex:
         return cache[k]
 
     def _sorted(self, mode: str):
-        if mode == 'tail-batch':
-            return self._k_hr, self._tails
-        if mode == 'head-batch':
-            return self._k_rt, self._heads
-        raise ValueError('negative batch mode %s not supported' % mode)
+        if mode not in ('tail-batch', 'head-batch'):
+            raise ValueError('negative batch mode %s not supported' % mode)
+        if self._on is not None:
+            return self._on[1][mode]
+        return (self._k_hr, self._tails) if mode == 'tail-batch' else (self._k_rt, self._heads)
 
     def _host_table_on(self, mode: str, dev):
         import torch
-        cand, vals = self._sorted(mode)
+        self._sorted(mode)  # (mode check)
+        cand, vals = (self._k_hr, self._tails) if mode == 'tail-batch' else (self._k_rt, self._heads)
         tag = '_tab_hr' if mode == 'tail-batch' else '_tab_rt'
         self._range(cand, np.zeros(1, dtype=np.int64), tag)  # builds the dense start table
         return (torch.from_numpy(getattr(self, tag).astype(np.int64)).to(dev),

@@ -513,7 +513,7 @@ class KGEModel(nn.Module):
 
         # Filtered MRR / MR / HITS@{1,3,10}: head-batch queries, then tail-batch
         # (model.py:349-418); the filter is dataloader.py:134-154's.
-        index = FilterIndex(all_true_triples, args.nentity, args.nrelation)
+        index = FilterIndex(all_true_triples, args.nentity, args.nrelation, device=dev)  # built on the GPU
         triples = triples_array(test_triples)
         desc = model.desc()
         ranks_seq = []  # head-batch queries, then tail-batch, as the reference's logs list
@@ -594,7 +594,7 @@ class KGEModel(nn.Module):
         (ranks, ties) tail)."""
         dev = ops._require_device(self.entity_embedding)
         index = all_true_triples if isinstance(all_true_triples, FilterIndex) else \
-            FilterIndex(all_true_triples, self.nentity, self.nrelation)
+            FilterIndex(all_true_triples, self.nentity, self.nrelation, device=dev)
         q = np.asarray(triples, dtype=np.int64).reshape(-1, 3)
         nq = len(q)
         outs = []
@@ -679,7 +679,7 @@ class KGEModel(nn.Module):
         default per `rank_trig`, see _rank_rotation)."""
         dev = ops._require_device(self.entity_embedding)
         index = all_true_triples if isinstance(all_true_triples, FilterIndex) else \
-            FilterIndex(all_true_triples, self.nentity, self.nrelation)
+            FilterIndex(all_true_triples, self.nentity, self.nrelation, device=dev)
         q = np.asarray(triples, dtype=np.int64).reshape(-1, 3)
         off, ids = index.filter_csr(q, mode)
         with torch.no_grad():

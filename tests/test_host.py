@@ -245,3 +245,23 @@ def test_filter_device_table_built_by_search_matches_host_table(monkeypatch):
         index.__dict__.pop("_dev_tables", None)
         assert tab.shape == (E * R + 1,) and tab.dtype == torch.int64
         assert torch.equal(tab, host_tab) and torch.equal(vals, host_vals), mode
+
+
+def test_filter_index_built_with_torch_matches_numpy():
+    """FilterIndex(..., device=...) builds the sorted key orders with torch
+    (test_step passes the GPU); its host arrays (made on first use), CSR
+    lists and dense tables equal the numpy-built index's (CPU device here)."""
+    from knowledgegraphembedding_amd import synth
+    from knowledgegraphembedding_amd.filters import FilterIndex
+    E, R = 400, 13
+    t = np.stack([synth.randint(41, (6000,), E), synth.randint(42, (6000,), R), synth.randint(43, (6000,), E)], 1)
+    ref = FilterIndex(t, E, R)
+    dev_idx = FilterIndex([tuple(map(int, x)) for x in t], E, R, device=torch.device("cpu"))
+    q = t[synth.randint(44, (300,), len(t))]
+    for mode in ("head-batch", "tail-batch"):
+        a, b = ref.device_table(mode, "cpu"), dev_idx.device_table(mode, "cpu")
+        assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1]), mode
+        (o1, i1), (o2, i2) = ref.filter_csr(q, mode), dev_idx.filter_csr(q, mode)
+        assert np.array_equal(o1, o2) and np.array_equal(i1, i2), mode
+    for n in ("_k_hr", "_tails", "_k_rt", "_heads"):
+        assert np.array_equal(getattr(ref, n), getattr(dev_idx, n)), n
