@@ -63,10 +63,7 @@ __global__ __launch_bounds__(256) void k_csr_fill(CsrArgs a) {
 // others' lane by lane (readlane) — ⌈m/64⌉²·64 register steps per bucket
 // instead of m global reads per id, which matters once buckets hold
 // hundreds of ids (the factor exchange's global batch).
-__global__ __launch_bounds__(256) void k_csr_rank_w(CsrArgs a, int64_t nb) {
-  const int lane = threadIdx.x & 63;
-  const int64_t b = (int64_t)blockIdx.x * 4 + wave_id();
-  if (b >= nb) return;
+__device__ __forceinline__ void csr_rank_bucket(const CsrArgs& a, int64_t b, int lane) {
   const int32_t b0 = a.off[b], b1 = a.off[b + 1];
   for (int32_t c0 = b0; c0 < b1; c0 += 64) {
     const bool mine = c0 + lane < b1;
@@ -79,6 +76,11 @@ __global__ __launch_bounds__(256) void k_csr_rank_w(CsrArgs a, int64_t nb) {
     }
     if (mine) a.occ[b0 + r] = v;
   }
+}
+__global__ __launch_bounds__(256) void k_csr_rank_w(CsrArgs a, int64_t nb) {
+  const int lane = threadIdx.x & 63;
+  for (int64_t b = (int64_t)blockIdx.x * 4 + wave_id(); b < nb; b += (int64_t)gridDim.x * 4)
+    csr_rank_bucket(a, b, lane);
 }
 
 __global__ __launch_bounds__(256) void k_rel_rows(RelArgs a) {
@@ -184,14 +186,23 @@ size_t csr_scan_temp_bytes(int64_t nb) {
 int launch_csr(const CsrArgs& a, hipStream_t s) {
   const int64_t nb = a.E + a.R;
   const int64_t N = a.Bn + 3 * a.B;
+  // (grids capped at 32 / 128 / 512 blocks, to leave k_row more CU slots,
+  // measured 0.697 / 0.578 / 0.559-0.560 ms per step against 0.561: the CSR
+  // has to finish inside k_row's window; profiles/r06/csr/bench_cap*.json)
+  const unsigned gk = grid_for(N);
+  const unsigned gb = (unsigned)((nb + 3) / 4);
   hipError_t e = hipMemsetAsync(a.cnt, 0, sizeof(int32_t) * (nb + 1), s);
   if (e != hipSuccess) return (int)e;
-  hipLaunchKernelGGL(k_csr_hist, dim3(grid_for(N)), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(k_csr_hist, dim3(gk), dim3(256), 0, s, a);
+  // (one-workgroup scan measured instead: no gain at FB15k, 469.5-471.1 vs
+  // 470.5-471.9 M triples/s, and 0.19 ms of join at YAGO3-10's 123 k buckets;
+  // its launch, like rocPRIM's, shows ≈210 µs beside k_row: waiting for a
+  // slot, not working; profiles/r06/csr/)
   size_t bytes = a.scan_tmp_bytes;
   e = rocprim::exclusive_scan(a.scan_tmp, bytes, a.cnt, a.off, int32_t(0), (size_t)nb + 1, rocprim::plus<int32_t>(), s);
   if (e != hipSuccess) return (int)e;
-  hipLaunchKernelGGL(k_csr_fill, dim3(grid_for(N)), dim3(256), 0, s, a);
-  hipLaunchKernelGGL(k_csr_rank_w, dim3((unsigned)((nb + 3) / 4)), dim3(256), 0, s, a, nb);
+  hipLaunchKernelGGL(k_csr_fill, dim3(gk), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(k_csr_rank_w, dim3(gb), dim3(256), 0, s, a, nb);
   return (int)hipGetLastError();
 }
 
