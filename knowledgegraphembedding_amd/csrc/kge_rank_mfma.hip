@@ -607,7 +607,10 @@ __device__ __forceinline__ bool xcd_tile(const XArgs& a, int& x, int& y) {
 // the lo·lo product, and (round 5) the same tile on v_mfma_f32_16x16x32_bf16
 // (each MFMA over a 32-k slab pair, 4 × 4 blocks of 16 × 16 per wave, 199
 // VGPRs, two workgroups per CU: DistMult 399-404 against 374-375 µs, ComplEx
-// 705-714 against 711-712, profiles/r05/rank/ab_tile_16x16x32_rejected.txt).
+// 705-714 against 711-712, profiles/r05/rank/ab_tile_16x16x32_rejected.txt),
+// and (round 6) two slabs per ring stage in a 2-stage ring — half the
+// barriers and DMA waits, two workgroups per CU in the same 64 KB: 875 against
+// 773 µs per two-direction DistMult launch (profiles/r06/rank_tile/).
 // s_waitcnt vmcnt(n) for the DMA counts of the ring (n = younger slabs × CPW)
 __device__ __forceinline__ void wait_vmcnt_dma(int n) {
   switch (n) {
