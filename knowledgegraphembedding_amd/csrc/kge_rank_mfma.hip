@@ -610,7 +610,9 @@ __device__ __forceinline__ bool xcd_tile(const XArgs& a, int& x, int& y) {
 // 705-714 against 711-712, profiles/r05/rank/ab_tile_16x16x32_rejected.txt),
 // and (round 6) two slabs per ring stage in a 2-stage ring — half the
 // barriers and DMA waits, two workgroups per CU in the same 64 KB: 875 against
-// 773 µs per two-direction DistMult launch (profiles/r06/rank_tile/).
+// 773 µs per two-direction DistMult launch — and a 2-stage one-slab ring (one
+// slab in flight, 37 KB, four workgroups per CU): 798 against 767 µs
+// (profiles/r06/rank_tile/).
 // s_waitcnt vmcnt(n) for the DMA counts of the ring (n = younger slabs × CPW)
 __device__ __forceinline__ void wait_vmcnt_dma(int n) {
   switch (n) {
